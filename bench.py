@@ -1,0 +1,182 @@
+"""Benchmark of the batched GKArray ingest path on MI355X.
+
+Metric (BASELINE.json): values ingested/sec (node) @1M streams eps=0.01, plus
+the fraction of the HBM roofline reached by the dominant kernel (k_ingest).
+
+Workload (BASELINE.json configs[2], the metric's configuration, which fits one
+GPU): 1,000,000 streams x 1,000 Pareto(1.5)+1 float64 values per GPU, eps=0.01.
+One step = reset every sketch, ingest the whole batch (k_stats + k_ingest: 9
+automatic flushes per stream at the reference's flush points) and answer
+quantiles([0.5, 0.9, 0.99]) for every stream (which flushes the 91 pending
+values first, gk:197).  Inputs are generated on the GPU (synthetic, seeded)
+and are resident in HBM before the timed region.  Multi-GPU: every rank runs
+its own 1M-stream shard (streams are independent: weak scaling, no collective
+on the data path); value = all ranks' values / max-over-ranks time.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "sketches-py_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, MI355X_MICROARCH.md "Chip-level parameters"
+HEADER_BYTES = 36       # per stream touched by k_ingest: slot1, n, E, pend read + n, E, pend written
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--streams", type=int, default=1_000_000, help="streams per GPU")
+    ap.add_argument("--values", type=int, default=1000, help="values per stream")
+    ap.add_argument("--eps", type=float, default=0.01)
+    ap.add_argument("--seed", type=int, default=3)
+    ap.add_argument("--cpu-sample", type=int, default=100000,
+                    help="streams of the same workload timed on the host oracle (rank 0, N=1)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, os.cpu_count())")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def make_input(S, L, seed, device):
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    u = torch.rand(S * L, dtype=torch.float64, device=device, generator=g)
+    x = (1.0 - u).pow_(-1.0 / 1.5)  # numpy pareto(1.5) + 1 by inversion
+    del u
+    offs = torch.arange(0, S * L + 1, L, dtype=torch.int64, device=device)
+    return x, offs
+
+
+def algorithmic_bytes(ss, S, N):
+    """Bytes one k_ingest launch must move on a fresh batch:
+    8 B per value + offsets + per stream 16 B per table entry read and written
+    + 8 B per pending value read and written + the header words."""
+    st = ss.stats()
+    e_out = int(st["size"].to(torch.int64).sum().item())
+    p_out = int(st["pending"].to(torch.int64).sum().item())
+    e_in = p_in = 0  # every step starts from reset sketches
+    return 8 * N + 8 * (S + 1) + 16 * (e_in + e_out) + 8 * (p_in + p_out) + HEADER_BYTES * S
+
+
+def cpu_baseline(x, L, sample, threads, eps, gpu_q):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from gk_oracle_c import OracleSet
+    xs = x[: sample * L].cpu().numpy()
+    offs = np.arange(0, sample * L + 1, L, dtype=np.int64)
+    o = OracleSet(sample, eps, threads=threads)
+    t0 = time.perf_counter()
+    o.ingest(xs, offs)
+    q = o.quantiles([0.5, 0.9, 0.99])
+    dt = time.perf_counter() - t0
+    same = np.array_equal(q.view(np.int64), gpu_q[:sample].view(np.int64))
+    return dict(value=sample * L / dt, unit="values/s", cores=threads, kind="port",
+                sample="%d streams x %d values (the first streams of the GPU workload), "
+                       "ingest + quantiles([.5,.9,.99]) in oracle/gk_oracle.c, %.1f s" % (sample, L, dt),
+                parity_on_sample=bool(same))
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    from gkarray_amd import StreamSet
+
+    S, L = a.streams, a.values
+    N = S * L
+    x, offs = make_input(S, L, a.seed + rank, dev)
+    ss = StreamSet(S, a.eps, device=dev)
+    qs = [0.5, 0.9, 0.99]
+
+    def step():
+        ss.reset()
+        ss.ingest(x, offs)
+        return ss.quantiles(qs)
+
+    # algorithmic bytes of one k_ingest launch (untimed)
+    ss.reset()
+    ss.ingest(x, offs)
+    bytes_per_launch = algorithmic_bytes(ss, S, N)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    ss.timing(True)
+    ss.read_timing()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        q = step()
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    flush_ms, stats_ms, launches = ss.read_timing()
+    ss.timing(False)
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    total_values = N * world * a.steps
+    value = total_values / dt
+    ms_step = dt / a.steps * 1e3
+    k_ms = flush_ms / max(launches, 1)
+    achieved = bytes_per_launch / (k_ms * 1e-3) / 1e9
+    line = {
+        "metric": "values ingested/sec (node) @1M streams eps=0.01; % of HBM roofline",
+        "value": value,
+        "unit": "values/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: Pareto(1.5)+1 float64 generated on GPU (seed %d + rank)" % a.seed,
+        "config": {"workload": "cfg3: %d streams x %d values per GPU, eps=%g, ingest + quantiles(.5,.9,.99)"
+                               % (S, L, a.eps),
+                   "streams_per_gpu": S, "values_per_stream": L, "eps": a.eps,
+                   "parallelism": "stream-sharded x%d (no collective)" % world},
+        "roofline": {"bound": "hbm", "kernel": "k_ingest", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "bytes_per_launch": bytes_per_launch, "launch_ms": k_ms,
+                     "stats_kernel_ms": stats_ms / max(launches, 1)},
+    }
+    if rank == 0 and world == 1 and not a.no_cpu:
+        threads = a.cpu_threads or min(16, os.cpu_count() or 1)
+        line["cpu_baseline"] = cpu_baseline(x, L, min(a.cpu_sample, S), threads, a.eps, q.cpu().numpy())
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,143 @@
+/*
+ * gk_capi.h -- C ABI of the MI355X-native batched GKArray engine.
+ *
+ * The reference (githomin/sketches-py, gkarray/gkarray.py, "gk:N" = line N) is a
+ * pure-Python class with no FFI.  This header is the boundary a ctypes (or cgo /
+ * JNI) binding binds; each entry point names the reference method it replaces.
+ * A "set" holds S independent GKArray streams that share one epsilon; every
+ * stream behaves exactly like one reference ``GKArray`` object fed the same
+ * values in the same order (tables and quantiles bit-exact).
+ *
+ * Conventions
+ *  - Every call returns an int status: GK_OK (0) or a negative GK_E_* code;
+ *    gk_last_error() returns a thread-local message for the last failure.
+ *  - Pointers documented "device" must be device memory on the set's GPU
+ *    (e.g. a torch tensor's data_ptr()); "host" pointers are host memory.
+ *  - `stream` is a hipStream_t passed as void* (NULL = the default stream).
+ *    Work is enqueued on it; calls that return host-visible scalars
+ *    (counts, errors) synchronise it before returning.
+ *  - A set is not thread-safe.  The library owns the set's device state;
+ *    callers own their input and output buffers.
+ */
+#ifndef GK_CAPI_H
+#define GK_CAPI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GK_OK 0
+#define GK_E_ARG (-1)          /* bad argument (size, pointer, NaN quantile ...)   */
+#define GK_E_EPS_MISMATCH (-2) /* merge of sets with different eps: gk:118-119     */
+#define GK_E_OVERFLOW (-3)     /* a stream's table exceeded the largest capacity  */
+#define GK_E_HIP (-4)          /* HIP runtime failure                              */
+#define GK_E_NOMEM (-5)        /* device allocation failed                          */
+#define GK_E_UNSUPPORTED (-6)  /* eps outside the supported range                  */
+
+typedef struct gk_set gk_set;
+
+/* Library / ABI version (major*10000 + minor*100 + patch). */
+int gk_version(void);
+
+/* Message for the last failed call on this thread ("" if none). */
+const char* gk_last_error(void);
+
+/* GKArray(eps) for `num_streams` streams (gk:21-29): empty tables, n=0,
+ * min=+inf, max=-inf, sum=avg=0.  `device` is the HIP device ordinal.
+ * `cap_hint` (0 = default) is the per-stream table capacity of the fast path;
+ * streams whose table outgrows it are promoted to a larger class
+ * automatically. */
+int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device,
+              gk_set** out);
+int gk_destroy(gk_set* set);
+
+/* Reset every stream to the freshly constructed state (gk:21-29). */
+int gk_reset(gk_set* set, void* stream);
+
+/* Batched GKArray.add (gk:49-61): stream s receives, in order,
+ * values[offsets[s] .. offsets[s+1]).  `values` (float64, device) and
+ * `offsets` (int64[num_streams+1], device, non-decreasing) describe a CSR
+ * batch over ALL streams of the set.  Flushes (merge_compress, gk:63-109)
+ * happen at exactly the reference's flush points (n % (int(1/eps)+1) == 0). */
+int gk_ingest(gk_set* set, const double* values, const int64_t* offsets,
+              void* stream);
+
+/* GKArray.merge_compress() with no argument (gk:63-109) on every stream that
+ * has pending values -- what size()/quantile()/quantiles() do first
+ * (gk:45-46, 166-167, 197-198). */
+int gk_flush(gk_set* set, void* stream);
+
+/* Batched GKArray.quantiles(qs) (gk:187-232) for every stream.
+ * `qs` (host, nq float64 values, no NaN); `out` (device, float64[S*nq],
+ * row-major [stream][q]).  Pending values are flushed first (mutation, as in
+ * the reference).  mode GK_Q_LIST = quantiles() semantics (the caller passes
+ * qs as given; if they are not sorted the per-q quantile() result is used,
+ * exactly as gk:205-206 does); mode GK_Q_SINGLE = quantile(q) semantics for
+ * every q (gk:156-185). */
+#define GK_Q_LIST 0
+#define GK_Q_SINGLE 1
+int gk_quantiles(gk_set* set, const double* qs, int nq, double* out, int mode,
+                 void* stream);
+
+/* Per-stream accessors num_values/_min/_max/sum/avg (gk:35-42, 25-29) and the
+ * table size len(entries) / pending count len(incoming) WITHOUT flushing.
+ * Any pointer may be NULL.  All outputs are device arrays of length S. */
+int gk_stats(gk_set* set, int64_t* n, double* mn, double* mx, double* sum,
+             double* avg, int32_t* table_size, int32_t* pending, void* stream);
+
+/* GKArray.merge(other) (gk:111-154), stream by stream, as the left fold
+ * dst.merge(srcs[0]); dst.merge(srcs[1]); ...  Like the reference it mutates
+ * each source (flushes its pending values, gk:126, 137).  Returns
+ * GK_E_EPS_MISMATCH if any eps differs (gk:118-119) or GK_E_ARG if the
+ * stream counts differ. */
+int gk_merge(gk_set* dst, gk_set* const* srcs, int nsrcs, void* stream);
+
+/* GKArray.merge_compress(entries) with an explicit entry list (gk:63-109,
+ * gk:71): stream s merges extra records [eoffs[s], eoffs[s+1]) given as
+ * (v, g, d) device arrays, each list sorted by v as the reference requires of
+ * its Entry lists. */
+int gk_merge_compress(gk_set* set, const double* v, const int32_t* g,
+                      const int32_t* d, const int64_t* eoffs, void* stream);
+
+/* Table export (the reference's `entries`, gk:23): writes per-stream table
+ * sizes to `sizes` (device int32[S]); then gk_export copies stream s's table
+ * to v/g/d[offs[s] ..] where offs (device int64[S+1]) is the caller's
+ * exclusive scan of those sizes.  Pending values (`incoming`, gk:24) go the
+ * same way with gk_export_pending_sizes / gk_export_pending. */
+int gk_export_sizes(gk_set* set, int32_t* sizes, void* stream);
+int gk_export(gk_set* set, const int64_t* offs, double* v, int32_t* g,
+              int32_t* d, void* stream);
+int gk_export_pending_sizes(gk_set* set, int32_t* sizes, void* stream);
+int gk_export_pending(gk_set* set, const int64_t* poffs, double* pv,
+                      void* stream);
+
+/* Import full per-stream state (checkpoint / RCCL payload): tables in CSR
+ * (offs, v, g, d), pending values in CSR (poffs, pv) and the header arrays
+ * (n, mn, mx, sum, avg), all device arrays of the set's S streams. */
+int gk_import(gk_set* set, const int64_t* offs, const double* v,
+              const int32_t* g, const int32_t* d, const int64_t* poffs,
+              const double* pv, const int64_t* n, const double* mn,
+              const double* mx, const double* sum, const double* avg,
+              void* stream);
+
+/* Introspection for tests and benchmarks. */
+int64_t gk_num_streams(const gk_set* set);
+double gk_eps(const gk_set* set);
+int gk_flush_period(const gk_set* set);       /* int(1.0/eps) + 1 (gk:60)  */
+int gk_capacity(const gk_set* set, int cls);  /* table capacity of a class */
+int64_t gk_num_promoted(const gk_set* set);   /* streams in the large class */
+
+/* Kernel timing: when enabled, gk_ingest records HIP events around the flush
+ * kernel it launches on `stream`; gk_timing_read returns the summed
+ * milliseconds and the number of launches since the last read. */
+int gk_timing_enable(gk_set* set, int on);
+int gk_timing_read(gk_set* set, double* flush_ms, double* stats_ms,
+                   int64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GK_CAPI_H */

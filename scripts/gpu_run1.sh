@@ -1,0 +1,11 @@
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/r1_pytest.log 2>&1
+rc=$?
+echo "pytest rc=$rc"
+tail -30 gpurun_out/r1_pytest.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 300 python bench.py --streams 100000 --steps 3 --warmup 1 --no-cpu > gpurun_out/r1_bench_small.log 2>&1 || exit $?
+cat gpurun_out/r1_bench_small.log
+timeout -k 10 400 python bench.py --steps 3 --warmup 1 > gpurun_out/r1_bench.log 2>&1 || exit $?
+cat gpurun_out/r1_bench.log

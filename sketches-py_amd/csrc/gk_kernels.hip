@@ -1,0 +1,1140 @@
+// gk_kernels.hip -- CDNA4 (gfx950) kernels of the batched GKArray engine.
+//
+// Reference: githomin/sketches-py gkarray/gkarray.py ("gk:N" = line N).
+// Every kernel reproduces the reference's integer decisions and float64
+// comparisons exactly ("Bit-exactness").  Built with
+// -ffp-contract=off: no FMA contraction of the reference's float64 formulas.
+//
+// Kernels
+//   k_stats      gk:52-59   lane per stream: n/_sum/_avg sequential chain, min/max
+//   k_ingest     gk:60-109  wave per stream: flush schedule + closed-form
+//                           merge_compress of each flush, table kept in LDS
+//                           for the whole call
+//   k_quantiles  gk:156-232 wave per stream: rank walk as a count over the
+//                           running max of prefix(g)+delta; small-n percentile
+//   k_merge      gk:111-154 wave per stream: convert `other`, stable merge of
+//                           the incoming list, general four-rule walk (gk:76-106)
+//   k_export / k_import / k_reset: state movement
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+#include "gk_state.h"
+#include "gk_launch.h"
+
+#define GK_KEEP_BIT 0x40000000
+
+// Largest T handled with int32 arithmetic: T = floor(2 eps (n-1)) is clamped
+// here; it would need n > 2^30/(2 eps) values in ONE stream to matter.
+#define GK_T_CLAMP (1 << 30)
+
+__device__ __forceinline__ int gk_threshold(const GKState& st, int64_t n) {
+  // np.floor(2.0*self.eps*(self._n - 1))  (gk:70): (2.0*eps) * float(n-1)
+  double t = floor(st.two_eps * (double)(n - 1));
+  if (t > (double)GK_T_CLAMP) t = (double)GK_T_CLAMP;
+  if (t < -1.0) t = -1.0;
+  return (int)t;
+}
+
+__device__ __forceinline__ int clampi(int x, int lo, int hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
+// ---------------------------------------------------------------------------
+// wave helpers (wave64)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+__device__ __forceinline__ int64_t wave_incl_scan_i64(int64_t v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int64_t t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+__device__ __forceinline__ int64_t wave_incl_max_i64(int64_t v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int64_t t = __shfl_up(v, o, 64);
+    if (lane >= o && t > v) v = t;
+  }
+  return v;
+}
+
+__device__ __forceinline__ int wave_sum_i32(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ===========================================================================
+// k_stats: gk:52-59 for every value, one lane per stream (the _sum/_avg
+// updates are a dependent float64 chain in insertion order, so a stream's
+// chain stays on one lane; 64 streams run side by side in a wave).
+// The header n is NOT written here: k_ingest owns n and runs after this
+// kernel on the same HIP stream, so both read the pre-call n.
+// ===========================================================================
+__global__ __launch_bounds__(256) void k_stats(GKState st, const double* __restrict__ x,
+                                               const int64_t* __restrict__ offs) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= st.S) return;
+  const int64_t o = offs[s], L = offs[s + 1] - o;
+  if (L <= 0) return;
+  int64_t n = st.n[s];
+  double mn = st.mn[s], mx = st.mx[s], sm = st.sum[s], av = st.avg[s];
+  const double* p = x + o;
+  for (int64_t i = 0; i < L; ++i) {
+    const double v = p[i];
+    n += 1;                               // gk:52
+    sm = sm + v;                          // gk:53
+    av = av + (v - av) * (1.0 / (double)n);  // gk:54 (no FMA: -ffp-contract=off)
+    if (v < mn) mn = v;                   // gk:56-57 (strict: first occurrence kept)
+    if (v > mx) mx = v;                   // gk:58-59
+  }
+  st.mn[s] = mn;
+  st.mx[s] = mx;
+  st.sum[s] = sm;
+  st.avg[s] = av;
+}
+
+// ===========================================================================
+// k_ingest: the add-driven flush path.
+//
+// One wave owns one stream for the whole call.  The stream's table is loaded
+// into LDS once, every flush of the call (gk:60-61: when n % P == 0) runs
+// against it there, and the final table is written back once.
+//
+// A flush (merge_compress with only raw pending values, gk:63-109) is
+// evaluated in closed form: every pending value x
+// is placed in gap j = #{entries <= x}; with m_j values in gap j and an
+// integer carry c from a removed predecessor,
+//     G = g_j + c + k,   k = clamp(T - d_j - (g_j + c), 0, m_j)
+// the k smallest gap values are absorbed into entry j (rule R3 true branch),
+// the remaining m_j - k are emitted as (x, 1, G + d_j - 1) (R3 false branch),
+// and entry j is removed (carry G) iff G + g_{j+1} + d_{j+1} <= T (R1/R4).
+// The tail (values >= the last entry, rule R2) is cut into chunks of
+// max(T,1) values, each emitting (last value, chunk size, 0).
+// ===========================================================================
+// Working storage of one flush: table double buffer, per-gap scratch and the
+// pending values grouped by gap.  LDS for the 256/2048 classes, a per-block
+// global-memory workspace for the largest class (same code, address space
+// known at compile time so LDS accesses stay ds_* instructions).
+struct FlushBuf {
+  double* tv[2];     // table values, double-buffered (old -> new)
+  int32_t* tg[2];
+  int32_t* td[2];
+  uint32_t* gpk;     // per gap: count, then packed (gap base << 16) | out base
+  int32_t* gk;       // per entry: absorbed count k | KEEP bit
+  int32_t* gdel;     // per entry: G, then delta of emitted gap values G+d-1
+  double* mv;        // pending values grouped by gap (unsorted inside a gap)
+  int32_t* mi;       // their insertion indices (stable tie-break, gk:72)
+};
+
+template <int CAP, int VPL>
+struct FlushLDS {
+  double tv[2][CAP];
+  int32_t tg[2][CAP];
+  int32_t td[2][CAP];
+  uint32_t gpk[CAP + 1];
+  int32_t gk[CAP + 1];
+  int32_t gdel[CAP + 1];
+  double mv[64 * VPL];
+  int32_t mi[64 * VPL];
+};
+
+// bytes of one block's global workspace for capacity `cap`
+__host__ __device__ inline size_t gk_flush_ws_bytes(int cap, int vpl) {
+  size_t b = 2 * (size_t)cap * 8 + 4 * (size_t)cap * 4 + 3 * ((size_t)cap + 1) * 4 + 64 * (size_t)vpl * 12;
+  return (b + 255) & ~(size_t)255;
+}
+
+__device__ inline FlushBuf flush_buf_global(unsigned char* base, int cap, int vpl) {
+  FlushBuf b;
+  double* dp = (double*)base;
+  b.tv[0] = dp; dp += cap;
+  b.tv[1] = dp; dp += cap;
+  b.mv = dp; dp += 64 * vpl;
+  int32_t* ip = (int32_t*)dp;
+  b.tg[0] = ip; ip += cap;
+  b.tg[1] = ip; ip += cap;
+  b.td[0] = ip; ip += cap;
+  b.td[1] = ip; ip += cap;
+  b.gpk = (uint32_t*)ip; ip += cap + 1;
+  b.gk = ip; ip += cap + 1;
+  b.gdel = ip; ip += cap + 1;
+  b.mi = ip;
+  return b;
+}
+
+template <int CAP, int VPL>
+__device__ inline FlushBuf flush_buf_lds(FlushLDS<CAP, VPL>& L) {
+  FlushBuf b;
+  b.tv[0] = L.tv[0]; b.tv[1] = L.tv[1];
+  b.tg[0] = L.tg[0]; b.tg[1] = L.tg[1];
+  b.td[0] = L.td[0]; b.td[1] = L.td[1];
+  b.gpk = L.gpk; b.gk = L.gk; b.gdel = L.gdel; b.mv = L.mv; b.mi = L.mi;
+  return b;
+}
+
+// Returns the new table size, or -1 if it would exceed CAP (nothing is
+// written to the new buffer in that case).  `cur` selects the old buffer; on
+// success the new table is in buffer cur^1.
+template <int VPL>
+__device__ __forceinline__ int flush_wave(const FlushBuf& L, const int cap, const int cur, const int E,
+                                          const double (&xv)[VPL], const int cnt, const int T,
+                                          const int lane) {
+  const double* __restrict__ tv = L.tv[cur];
+  const int32_t* __restrict__ tg = L.tg[cur];
+  const int32_t* __restrict__ td = L.td[cur];
+  double* __restrict__ nv = L.tv[cur ^ 1];
+  int32_t* __restrict__ ng = L.tg[cur ^ 1];
+  int32_t* __restrict__ nd = L.td[cur ^ 1];
+
+  // ---- gap of each pending value: number of entries <= x (gk:93 '<' puts
+  //      a value equal to an entry after that entry) -------------------------
+  int xg[VPL];
+  const int top = E ? (1 << (31 - __clz(E))) : 0;
+#pragma unroll
+  for (int r = 0; r < VPL; ++r) {
+    int pos = 0;
+    const double x = xv[r];
+    for (int step = top; step > 0; step >>= 1) {
+      const int pr = pos + step;
+      if (pr <= E && tv[pr - 1] <= x) pos = pr;
+    }
+    xg[r] = pos;
+  }
+  for (int j = lane; j <= E; j += 64) L.gpk[j] = 0u;
+  __syncthreads();
+  uint32_t xs[VPL];
+#pragma unroll
+  for (int r = 0; r < VPL; ++r) {
+    const int i = lane + 64 * r;
+    xs[r] = (i < cnt) ? atomicAdd(&L.gpk[xg[r]], 1u) : 0u;
+  }
+  __syncthreads();
+
+  // ---- carry walk over the entries -----------------------------------------
+  // Lane l owns the contiguous block [l*K, l*K+K).  A lane can run its block
+  // once its carry-in is known: lane 0, or a lane whose predecessor entry is
+  // kept even with carry 0 (then it is kept for any carry, because G grows
+  // with c).  Remaining lanes wait for their left neighbour (rounds).
+  const int K = (E + 63) >> 6;
+  const int j0 = lane * K;
+  const int jend = min(j0 + K, E);
+  const bool has = j0 < E;
+  bool known = (lane == 0) || !has;
+  if (has && lane > 0) {
+    const int jp = j0 - 1;
+    const int g = tg[jp], d = td[jp], m = (int)L.gpk[jp];
+    const int G0 = g + clampi(T - d - g, 0, m);
+    known = !(G0 + tg[j0] + td[j0] <= T);
+  }
+  bool done = !has;
+  int cin = 0, cout = 0;
+  for (;;) {
+    if (known && !done) {
+      int c = cin;
+      for (int j = j0; j < jend; ++j) {
+        const int g = tg[j], d = td[j], m = (int)L.gpk[j];
+        const int Gp = g + c;
+        const int k = clampi(T - d - Gp, 0, m);
+        const int G = Gp + k;
+        const bool rem = (j + 1 < E) && (G + tg[j + 1] + td[j + 1] <= T);
+        L.gk[j] = k | (rem ? 0 : GK_KEEP_BIT);
+        L.gdel[j] = G;
+        c = rem ? G : 0;
+      }
+      cout = c;
+      done = true;
+    }
+    const int pc = __shfl_up(cout, 1, 64);
+    const int pd = __shfl_up((int)done, 1, 64);
+    if (!known && pd) {
+      known = true;
+      cin = pc;
+    }
+    if (__all(done)) break;
+  }
+
+  // ---- output counts: gap j emits m_j - k_j values, then entry j if kept;
+  //      the tail emits ceil(m_E / max(T,1)) chunk ends -----------------------
+  const int cs = T > 1 ? T : 1;
+  const int tail_lane = E == 0 ? 0 : (E - 1) / K;
+  uint32_t sm = 0, so = 0;
+  for (int j = j0; j < jend; ++j) {
+    const int m = (int)L.gpk[j];
+    const int kk = L.gk[j];
+    sm += (uint32_t)m;
+    so += (uint32_t)(m - (kk & ~GK_KEEP_BIT) + ((kk & GK_KEEP_BIT) ? 1 : 0));
+  }
+  int mE = 0;
+  if (lane == tail_lane) {
+    mE = (int)L.gpk[E];
+    sm += (uint32_t)mE;
+    so += (uint32_t)((mE + cs - 1) / cs);
+  }
+  const uint32_t incl = wave_incl_scan_u32((sm << 16) | so, lane);
+  const uint32_t total = __shfl(incl, 63, 64);
+  const int newE = (int)(total & 0xffffu);
+  if (newE > cap) return -1;
+  uint32_t base = incl - ((sm << 16) | so);
+  for (int j = j0; j < jend; ++j) {
+    const int m = (int)L.gpk[j];
+    const int kk = L.gk[j];
+    const int k = kk & ~GK_KEEP_BIT;
+    const int G = L.gdel[j];
+    const int d = td[j];
+    L.gpk[j] = base;
+    L.gdel[j] = G + d - 1;
+    const int ob = (int)(base & 0xffffu);
+    if (kk & GK_KEEP_BIT) {
+      const int pos = ob + m - k;
+      nv[pos] = tv[j];
+      ng[pos] = G;
+      nd[pos] = d;
+    }
+    base += ((uint32_t)m << 16) | (uint32_t)(m - k + ((kk & GK_KEEP_BIT) ? 1 : 0));
+  }
+  if (lane == tail_lane) L.gpk[E] = base;
+  const int totm = (int)(total >> 16);
+  __syncthreads();
+
+  // ---- stable order inside each gap, then emit the surviving values --------
+#pragma unroll
+  for (int r = 0; r < VPL; ++r) {
+    const int i = lane + 64 * r;
+    if (i < cnt) {
+      const int pos = (int)(L.gpk[xg[r]] >> 16) + (int)xs[r];
+      L.mv[pos] = xv[r];
+      L.mi[pos] = i;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < VPL; ++r) {
+    const int i = lane + 64 * r;
+    if (i < cnt) {
+      const int gap = xg[r];
+      const uint32_t pk = L.gpk[gap];
+      const int gb = (int)(pk >> 16);
+      const int ge = gap < E ? (int)(L.gpk[gap + 1] >> 16) : totm;
+      const double x = xv[r];
+      int rk = 0;
+      for (int t = gb; t < ge; ++t) {
+        const double y = L.mv[t];
+        rk += (y < x) || (y == x && L.mi[t] < i);
+      }
+      if (gap < E) {
+        const int k = L.gk[gap] & ~GK_KEEP_BIT;
+        if (rk >= k) {
+          const int pos = (int)(pk & 0xffffu) + rk - k;
+          nv[pos] = x;
+          ng[pos] = 1;
+          nd[pos] = L.gdel[gap];
+        }
+      } else {
+        const int m = ge - gb;
+        const int q = rk / cs;
+        const int rr = rk - q * cs;
+        if (rr == cs - 1 || rk == m - 1) {
+          const int pos = (int)(pk & 0xffffu) + q;
+          nv[pos] = x;
+          ng[pos] = rr + 1;
+          nd[pos] = 0;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  return newE;
+}
+
+// CAP > 0: LDS working storage of that capacity (class 256 / 2048).
+// CAP == 0: global workspace `ws` (ws_bytes per block) of capacity `cap`.
+// list == NULL: every class-0 stream; else the listed streams (class c > 0).
+template <int CAP, int VPL>
+__global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restrict__ x,
+                                               const int64_t* __restrict__ offs,
+                                               const int32_t* __restrict__ list, int64_t count,
+                                               int force, int cap, unsigned char* ws, size_t ws_bytes,
+                                               int32_t* __restrict__ ovf_count,
+                                               int32_t* __restrict__ ovf_list) {
+  constexpr int LCAP = CAP > 0 ? CAP : 1;
+  constexpr int LVPL = CAP > 0 ? VPL : 1;
+  __shared__ FlushLDS<LCAP, LVPL> Ls;
+  FlushBuf B;
+  if constexpr (CAP > 0) {
+    B = flush_buf_lds<LCAP, LVPL>(Ls);
+    cap = CAP;
+  } else {
+    B = flush_buf_global(ws + (size_t)blockIdx.x * ws_bytes, cap, VPL);
+  }
+  const int lane = threadIdx.x;
+  const int P = st.P;
+  for (int64_t w = blockIdx.x; w < count; w += gridDim.x) {
+    const int64_t s = list ? (int64_t)list[w] : w;
+    if (!list && st.cls[s] != 0) continue;  // promoted: handled by its class launch
+    int64_t xo = 0, Lx = 0;
+    if (x) {
+      xo = offs[s];
+      Lx = offs[s + 1] - xo;
+    }
+    int p = st.pend[s];
+    int64_t n = st.n[s];
+    // force 1: flush only if values are pending (size/quantile, gk:45, 166, 197)
+    // force 2: unconditional merge_compress() (merge, gk:122, 126, 137)
+    if (Lx <= 0 && !((force == 1 && p > 0) || (force == 2 && n > 0))) continue;
+    GKRec* __restrict__ tab = gk_table_ptr(st, s);
+    double* __restrict__ pb = st.pbuf + s * (int64_t)st.pmax;
+    int E = st.E[s];
+    int cur = 0;
+    for (int j = lane; j < E; j += 64) {
+      const GKRec rc = tab[j];
+      B.tv[0][j] = rc.v;
+      B.tg[0][j] = rc.g;
+      B.td[0][j] = rc.d;
+    }
+    __syncthreads();
+
+    bool ok = true;
+    int64_t used = 0;
+    int64_t need = P - (n % P);  // adds until n hits the next multiple of P (gk:60)
+    while (used + need <= Lx) {
+      const int cnt = p + (int)need;
+      double xv[VPL];
+#pragma unroll
+      for (int r = 0; r < VPL; ++r) {
+        const int i = lane + 64 * r;
+        xv[r] = (i < p) ? pb[i] : ((i < cnt) ? x[xo + used + (i - p)] : 0.0);
+      }
+      n += need;
+      const int nE = flush_wave<VPL>(B, cap, cur, E, xv, cnt, gk_threshold(st, n), lane);
+      if (nE < 0) {
+        ok = false;
+        break;
+      }
+      E = nE;
+      cur ^= 1;
+      used += need;
+      p = 0;
+      need = P;
+    }
+    if (ok) {
+      const int64_t rem = Lx - used;  // < need: no automatic flush for these
+      if ((force == 1 && p + rem > 0) || force == 2) {
+        const int cnt = p + (int)rem;
+        double xv[VPL];
+#pragma unroll
+        for (int r = 0; r < VPL; ++r) {
+          const int i = lane + 64 * r;
+          xv[r] = (i < p) ? pb[i] : ((i < cnt) ? x[xo + used + (i - p)] : 0.0);
+        }
+        n += rem;
+        const int nE = flush_wave<VPL>(B, cap, cur, E, xv, cnt, gk_threshold(st, n), lane);
+        if (nE < 0) {
+          ok = false;
+        } else {
+          E = nE;
+          cur ^= 1;
+          p = 0;
+        }
+      } else {
+        for (int64_t i = lane; i < rem; i += 64) pb[p + i] = x[xo + used + i];
+        p += (int)rem;
+        n += rem;
+      }
+    }
+    if (!ok) {
+      // nothing was written back: the stream keeps its pre-call state and
+      // is re-run by the host after promotion to the next capacity class
+      if (lane == 0) {
+        const int k = atomicAdd(ovf_count, 1);
+        ovf_list[k] = (int32_t)s;
+      }
+      __syncthreads();
+      continue;
+    }
+    for (int j = lane; j < E; j += 64) {
+      GKRec rc;
+      rc.v = B.tv[cur][j];
+      rc.g = B.tg[cur][j];
+      rc.d = B.td[cur][j];
+      tab[j] = rc;
+    }
+    if (lane == 0) {
+      st.n[s] = n;
+      st.E[s] = E;
+      st.pend[s] = p;
+    }
+    __syncthreads();
+  }
+}
+
+// ===========================================================================
+// k_quantiles: gk:156-232.  One wave per stream, table read straight from HBM.
+//   large n: the reference walks i = 0.. while prefix_g(i) + d_i - 1 <= rank
+//   + spread.  The first i that breaks is the number of i whose RUNNING MAX
+//   of prefix_g + d - 1 is <= rank + spread (the running max is monotone),
+//   so each q is one count over the table.
+//   small n (n < 1/eps, gk:169): numpy.percentile(values, q*100), linear.
+// mode 0 (quantiles, sorted qs): no break -> _max (gk:225-230)
+// mode 1 (quantile / unsorted qs): no break -> entries[-1].val (gk:185)
+// ===========================================================================
+__device__ __forceinline__ double gk_nan() { return __longlong_as_double(0x7ff8000000000000LL); }
+
+__device__ double percentile_linear(const GKRec* __restrict__ tab, int E, double q) {
+  // numpy 2.2.6 _function_base_impl.py: q/100 (l.4257), (n-1)*q (l.107),
+  // bounds (l.4748-4750), gamma (l.4632), _lerp (l.4653-4657)
+  const double qq = (q * 100.0) / 100.0;
+  const double vi = (double)(E - 1) * qq;
+  double prev;
+  double a, b;
+  if (vi >= (double)(E - 1)) {
+    prev = -1.0;
+    a = tab[E - 1].v;
+    b = a;
+  } else if (vi < 0.0) {
+    prev = 0.0;
+    a = tab[0].v;
+    b = a;
+  } else {
+    prev = floor(vi);
+    const int pi = (int)prev;
+    a = tab[pi].v;
+    b = tab[pi + 1].v;
+  }
+  const double gamma = vi - prev;
+  const double diff = b - a;
+  if (gamma >= 0.5) return b - diff * (1.0 - gamma);
+  return a + diff * gamma;
+}
+
+__global__ __launch_bounds__(64) void k_quantiles(GKState st, const double* __restrict__ qs, int nq,
+                                                  double* __restrict__ out, int mode) {
+  const int lane = threadIdx.x;
+  for (int64_t s = blockIdx.x; s < st.S; s += gridDim.x) {
+    double* o = out + s * (int64_t)nq;
+    const int64_t n = st.n[s];
+    const int E = st.E[s];
+    if (n == 0 || E == 0) {
+      for (int q = lane; q < nq; q += 64) o[q] = gk_nan();
+      continue;
+    }
+    const GKRec* __restrict__ tab = gk_table_ptr(st, s);
+    const double mn = st.mn[s], mx = st.mx[s];
+    if ((double)n < st.inv_eps) {  // gk:169 / gk:200
+      for (int q = lane; q < nq; q += 64) {
+        const double qv = qs[q];
+        o[q] = (qv >= 0.0 && qv <= 1.0) ? percentile_linear(tab, E, qv) : gk_nan();
+      }
+      continue;
+    }
+    const int K = (E + 63) >> 6;
+    const int j0 = lane * K;
+    const int jend = min(j0 + K, E);
+    int64_t bsum = 0;
+    for (int j = j0; j < jend; ++j) bsum += tab[j].g;
+    const int64_t bex = wave_incl_scan_i64(bsum, lane) - bsum;
+    // running max of prefix_g(i) + d_i - 1, block-local then across lanes
+    int64_t acc = bex, bmax = INT64_MIN;
+    for (int j = j0; j < jend; ++j) {
+      const GKRec rc = tab[j];
+      acc += rc.g;
+      const int64_t a = acc + rc.d - 1;
+      if (a > bmax) bmax = a;
+    }
+    const int64_t pmax_incl = wave_incl_max_i64(bmax, lane);
+    int64_t pmax_ex = __shfl_up(pmax_incl, 1, 64);
+    if (lane == 0) pmax_ex = INT64_MIN;
+    const int64_t spread = (int64_t)(st.eps * (double)(n - 1));  // gk:174 / gk:210
+    for (int q = 0; q < nq; ++q) {
+      const double qv = qs[q];
+      const bool valid = (qv >= 0.0 && qv <= 1.0);
+      const int64_t rank = valid ? (int64_t)(qv * (double)(n - 1) + 1.0) : 0;  // gk:173
+      const int64_t th = rank + spread;
+      int c = 0;
+      int64_t run = pmax_ex, a2 = bex;
+      for (int j = j0; j < jend; ++j) {
+        const GKRec rc = tab[j];
+        a2 += rc.g;
+        const int64_t a = a2 + rc.d - 1;
+        if (a > run) run = a;
+        c += (run <= th) ? 1 : 0;
+      }
+      const int i = wave_sum_i32(c);
+      if (lane == 0) {
+        double r;
+        if (!valid) r = gk_nan();
+        else if (i == 0) r = mn;                         // gk:182-183 / gk:220
+        else if (i < E) r = tab[i - 1].v;                // gk:185 / gk:220
+        else r = (mode == 0) ? mx : tab[E - 1].v;        // gk:229 / gk:185
+        o[q] = r;
+      }
+    }
+  }
+}
+
+// ===========================================================================
+// k_merge: GKArray.merge (gk:111-154) and merge_compress(entries), stream by
+// stream.  The incoming list (self's raw pending values, then the converted
+// records of `other` or the caller's records) is stably ordered by value and
+// the four-rule walk of gk:76-106 runs on lane 0 over LDS: incoming records
+// carry g > 1 here, so the add-path closed form does not apply.
+// `other` has already been flushed by the caller (gk:126, gk:137).
+// ===========================================================================
+struct MergeArgs {
+  GKState dst;
+  GKState src;            // mode 0: the other set (already flushed, gk:126/137)
+  const double* ev;       // mode 1: explicit records (v, g, d) in CSR
+  const int32_t* eg;
+  const int32_t* ed;
+  const int64_t* eoffs;
+  int mode;               // 0 = merge(other), 1 = merge_compress(entries)
+  int cap;                // LDS capacity for tables / records
+  const int32_t* list;    // streams to process (NULL = all)
+  int64_t count;
+  int32_t* ovf_count;
+  int32_t* ovf_list;
+  unsigned char* ws;      // global workspace (largest class), NULL = dynamic LDS
+  size_t ws_bytes;        // per block
+};
+
+struct MergeLDS {
+  double *tv, *rv, *sp, *iv, *ov;
+  int32_t *tg, *td, *rg, *rd, *ig, *id, *og, *od;
+};
+
+__device__ __forceinline__ MergeLDS merge_carve(unsigned char* smem, int cap, int pm) {
+  const int MR = cap + 1, MI = cap + 1 + pm;
+  MergeLDS m;
+  double* dp = (double*)smem;
+  m.tv = dp; dp += cap;
+  m.rv = dp; dp += MR;
+  m.sp = dp; dp += pm;
+  m.iv = dp; dp += MI;
+  m.ov = dp; dp += cap;
+  int32_t* ip = (int32_t*)dp;
+  m.tg = ip; ip += cap;
+  m.td = ip; ip += cap;
+  m.rg = ip; ip += MR;
+  m.rd = ip; ip += MR;
+  m.ig = ip; ip += MI;
+  m.id = ip; ip += MI;
+  m.og = ip; ip += cap;
+  m.od = ip; ip += cap;
+  return m;
+}
+
+__device__ __forceinline__ void flag_overflow(int32_t* cnt, int32_t* list, int64_t s, int lane) {
+  if (lane == 0) {
+    const int k = atomicAdd(cnt, 1);
+    list[k] = (int32_t)s;
+  }
+}
+
+template <bool GLOBAL>
+__global__ __launch_bounds__(64) void k_merge(MergeArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ int sh_out;
+  const int lane = threadIdx.x;
+  const int CAPL = a.cap;
+  const int PM = a.dst.pmax;
+  unsigned char* base = GLOBAL ? a.ws + (size_t)blockIdx.x * a.ws_bytes : smem;
+  const MergeLDS m = merge_carve(base, CAPL, PM);
+  const GKState& st = a.dst;
+  for (int64_t w = blockIdx.x; w < a.count; w += gridDim.x) {
+    const int64_t s = a.list ? (int64_t)a.list[w] : w;
+    GKRec* __restrict__ tab = gk_table_ptr(st, s);
+    const int outcap = min(st.cap[st.cls[s]], CAPL);
+    int64_t n = st.n[s];
+    const int E = st.E[s];
+    const int p = st.pend[s];
+    const double* __restrict__ pb = st.pbuf + s * (int64_t)st.pmax;
+
+    // ---- branch of gk:121-133 -------------------------------------------------
+    int nrec = 0;
+    if (a.mode == 0) {
+      const GKState& os = a.src;
+      const int64_t on = os.n[s];
+      const int oE = os.E[s];
+      const GKRec* __restrict__ otab = gk_table_ptr(os, s);
+      if (on != 0 && n == 0) {  // gk:125-133: take a copy of (flushed) other
+        if (oE > outcap) {
+          flag_overflow(a.ovf_count, a.ovf_list, s, lane);
+          __syncthreads();
+          continue;
+        }
+        for (int j = lane; j < oE; j += 64) tab[j] = otab[j];
+        if (lane == 0) {
+          st.n[s] = on;
+          st.E[s] = oE;
+          st.pend[s] = 0;
+          st.mn[s] = os.mn[s];
+          st.mx[s] = os.mx[s];
+          st.sum[s] = os.sum[s];
+          st.avg[s] = os.avg[s];
+        }
+        __syncthreads();
+        continue;
+      }
+      if (on != 0) {
+        // gk:136-147: spread from other's n, then the converted records
+        //   (other._min, g0+d0-spread-1), (v_k, g_{k+1}+d_{k+1}-d_k),
+        //   (v_{L-1}, spread+1-d_{L-1}); only g > 0 is kept.
+        const int64_t spread = (int64_t)(os.eps * (double)(on - 1));
+        const int ncand = oE + 1;
+        if (ncand > CAPL + 1) {
+          flag_overflow(a.ovf_count, a.ovf_list, s, lane);
+          __syncthreads();
+          continue;
+        }
+        int base = 0;
+        for (int c0 = 0; c0 < ncand; c0 += 64) {
+          const int c = c0 + lane;
+          int64_t gv = 0;
+          double vv = 0.0;
+          if (c < ncand) {
+            if (c == 0) {
+              gv = (int64_t)otab[0].g + otab[0].d - spread - 1;
+              vv = os.mn[s];
+            } else if (c < oE) {
+              gv = (int64_t)otab[c].g + otab[c].d - otab[c - 1].d;
+              vv = otab[c - 1].v;
+            } else {
+              gv = spread + 1 - otab[oE - 1].d;
+              vv = otab[oE - 1].v;
+            }
+          }
+          const bool keep = (c < ncand) && gv > 0;
+          const unsigned long long bal = __ballot(keep);
+          const int before = __popcll(bal & ((1ull << lane) - 1ull));
+          if (keep) {
+            m.rv[base + before] = vv;
+            m.rg[base + before] = (int32_t)gv;
+            m.rd[base + before] = 0;
+          }
+          base += __popcll(bal);
+        }
+        nrec = base;
+        n += on;  // gk:149
+        if (lane == 0) {  // gk:151-152: min()/max() keep self's value on ties
+          const double omn = os.mn[s], omx = os.mx[s];
+          if (omn < st.mn[s]) st.mn[s] = omn;
+          if (omx > st.mx[s]) st.mx[s] = omx;
+        }
+      }
+      // on == 0: gk:121-123, self.merge_compress() with no records
+    } else {
+      const int64_t eo = a.eoffs[s];
+      nrec = (int)(a.eoffs[s + 1] - eo);
+      if (nrec > CAPL + 1) {
+        flag_overflow(a.ovf_count, a.ovf_list, s, lane);
+        __syncthreads();
+        continue;
+      }
+      for (int c = lane; c < nrec; c += 64) {
+        m.rv[c] = a.ev[eo + c];
+        m.rg[c] = a.eg[eo + c];
+        m.rd[c] = a.ed[eo + c];
+      }
+    }
+    if (E > CAPL) {
+      flag_overflow(a.ovf_count, a.ovf_list, s, lane);
+      __syncthreads();
+      continue;
+    }
+    // ---- stable order of self's raw pending values (gk:72) ------------------
+    for (int i = lane; i < p; i += 64) m.ov[i] = pb[i];
+    __syncthreads();
+    for (int i = lane; i < p; i += 64) {
+      const double x = m.ov[i];
+      int rk = 0;
+      for (int t = 0; t < p; ++t) {
+        const double y = m.ov[t];
+        rk += (y < x) || (y == x && t < i);
+      }
+      m.sp[rk] = x;
+    }
+    __syncthreads();
+    // ---- merged incoming list: `self.incoming + entries` sorted stably, so on
+    //      equal values the raw pending values come first (gk:71-72) ----------
+    for (int r = lane; r < p; r += 64) {
+      const double x = m.sp[r];
+      int lo = 0, hi = nrec;  // records strictly below x
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (m.rv[mid] < x) lo = mid + 1; else hi = mid;
+      }
+      m.iv[r + lo] = x;
+      m.ig[r + lo] = 1;
+      m.id[r + lo] = 0;
+    }
+    for (int t = lane; t < nrec; t += 64) {
+      const double y = m.rv[t];
+      int lo = 0, hi = p;  // pending values <= y
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (m.sp[mid] <= y) lo = mid + 1; else hi = mid;
+      }
+      m.iv[t + lo] = y;
+      m.ig[t + lo] = m.rg[t];
+      m.id[t + lo] = m.rd[t];
+    }
+    for (int j = lane; j < E; j += 64) {
+      const GKRec rc = tab[j];
+      m.tv[j] = rc.v;
+      m.tg[j] = rc.g;
+      m.td[j] = rc.d;
+    }
+    __syncthreads();
+    // ---- the four-rule walk of gk:76-106, on lane 0 ---------------------------
+    if (lane == 0) {
+      const int64_t T = (int64_t)floor(st.two_eps * (double)(n - 1));  // gk:70
+      const int M = p + nrec;
+      int i = 0, j = 0, no = 0;
+      bool of = false;
+      while (i < M || j < E) {
+        bool emit = false;
+        double ev = 0.0;
+        int64_t eg = 0, ed = 0;
+        if (i < M && (j == E || m.iv[i] < m.tv[j])) {
+          if (j == E) {  // gk:85-92
+            if (i + 1 < M && (int64_t)m.ig[i] + m.ig[i + 1] + m.id[i + 1] <= T) {
+              m.ig[i + 1] += m.ig[i];
+            } else {
+              emit = true; ev = m.iv[i]; eg = m.ig[i]; ed = m.id[i];
+            }
+          } else {  // gk:93-99
+            if ((int64_t)m.ig[i] + m.tg[j] + m.td[j] <= T) {
+              m.tg[j] += m.ig[i];
+            } else {
+              emit = true; ev = m.iv[i]; eg = m.ig[i]; ed = (int64_t)m.tg[j] + m.td[j] - m.ig[i];
+            }
+          }
+          ++i;
+        } else {  // gk:77-84, gk:100-106
+          if (j + 1 < E && (int64_t)m.tg[j] + m.tg[j + 1] + m.td[j + 1] <= T) {
+            m.tg[j + 1] += m.tg[j];
+          } else {
+            emit = true; ev = m.tv[j]; eg = m.tg[j]; ed = m.td[j];
+          }
+          ++j;
+        }
+        if (emit) {
+          if (no >= outcap) { of = true; break; }
+          m.ov[no] = ev; m.og[no] = (int32_t)eg; m.od[no] = (int32_t)ed; ++no;
+        }
+      }
+      sh_out = of ? -1 : no;
+    }
+    __syncthreads();
+    const int no = sh_out;
+    if (no < 0) {
+      flag_overflow(a.ovf_count, a.ovf_list, s, lane);
+      __syncthreads();
+      continue;
+    }
+    for (int j = lane; j < no; j += 64) {
+      GKRec rc;
+      rc.v = m.ov[j];
+      rc.g = m.og[j];
+      rc.d = m.od[j];
+      tab[j] = rc;
+    }
+    if (lane == 0) {
+      st.n[s] = n;
+      st.E[s] = no;
+      st.pend[s] = 0;
+    }
+    __syncthreads();
+  }
+}
+
+// ===========================================================================
+// state movement
+// ===========================================================================
+__global__ void k_reset(GKState st) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= st.S) return;
+  st.n[s] = 0;
+  st.E[s] = 0;
+  st.pend[s] = 0;
+  st.mn[s] = __longlong_as_double(0x7ff0000000000000LL);   // +inf (gk:25)
+  st.mx[s] = __longlong_as_double((long long)0xfff0000000000000ULL);  // -inf (gk:26)
+  st.sum[s] = 0.0;
+  st.avg[s] = 0.0;
+}
+
+__global__ void k_export(GKState st, const int64_t* __restrict__ offs, double* __restrict__ v,
+                         int32_t* __restrict__ g, int32_t* __restrict__ d) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t s = wave; s < st.S; s += nw) {
+    const GKRec* tab = gk_table_ptr(st, s);
+    const int E = st.E[s];
+    const int64_t o = offs[s];
+    for (int j = lane; j < E; j += 64) {
+      const GKRec rc = tab[j];
+      if (v) v[o + j] = rc.v;
+      if (g) g[o + j] = rc.g;
+      if (d) d[o + j] = rc.d;
+    }
+  }
+}
+
+__global__ void k_export_pending(GKState st, const int64_t* __restrict__ offs, double* __restrict__ v) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t s = wave; s < st.S; s += nw) {
+    const int p = st.pend[s];
+    const double* pb = st.pbuf + s * (int64_t)st.pmax;
+    const int64_t o = offs[s];
+    for (int j = lane; j < p; j += 64) v[o + j] = pb[j];
+  }
+}
+
+__global__ void k_import(GKState st, const int64_t* __restrict__ offs, const double* __restrict__ v,
+                         const int32_t* __restrict__ g, const int32_t* __restrict__ d,
+                         const int64_t* __restrict__ poffs, const double* __restrict__ pv,
+                         int32_t* __restrict__ ovf_count, int32_t* __restrict__ ovf_list) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t s = wave; s < st.S; s += nw) {
+    const int cap = st.cap[st.cls[s]];
+    const int64_t o = offs[s];
+    const int E = (int)(offs[s + 1] - o);
+    const int64_t po = poffs[s];
+    const int p = (int)(poffs[s + 1] - po);
+    if (E > cap || p > st.pmax) {
+      if (lane == 0) {
+        const int k = atomicAdd(ovf_count, 1);
+        ovf_list[k] = (int32_t)s;
+      }
+      continue;
+    }
+    GKRec* tab = gk_table_ptr(st, s);
+    for (int j = lane; j < E; j += 64) {
+      GKRec rc;
+      rc.v = v[o + j];
+      rc.g = g[o + j];
+      rc.d = d[o + j];
+      tab[j] = rc;
+    }
+    double* pb = st.pbuf + s * (int64_t)st.pmax;
+    for (int j = lane; j < p; j += 64) pb[j] = pv[po + j];
+    if (lane == 0) {
+      st.E[s] = E;
+      st.pend[s] = p;
+    }
+  }
+}
+
+// move each listed stream's table into its (already assigned) slot of class `ncls`
+__global__ void k_promote(GKState st, const int32_t* __restrict__ list, int64_t count,
+                          const int32_t* __restrict__ slots, int ncls) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t w = wave; w < count; w += nw) {
+    const int64_t s = list[w];
+    const int32_t slot = slots[w];
+    const GKRec* src = gk_table_ptr(st, s);
+    GKRec* dst = st.tab[ncls] + (int64_t)slot * st.cap[ncls];
+    const int E = st.E[s];
+    for (int j = lane; j < E; j += 64) dst[j] = src[j];
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+      st.cls[s] = ncls;
+      st.slot[s] = slot;
+    }
+  }
+}
+
+// ===========================================================================
+// host-side launchers (called from gk_capi.cpp)
+// ===========================================================================
+static int g_num_cu = 0;
+
+static int num_cu() {
+  if (g_num_cu == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) == hipSuccess) g_num_cu = prop.multiProcessorCount;
+    if (g_num_cu <= 0) g_num_cu = 256;
+  }
+  return g_num_cu;
+}
+
+int gk_num_cu() { return num_cu(); }
+
+template <int CAP, int VPL>
+static hipError_t launch_ingest_t(const GKState& st, const double* x, const int64_t* offs,
+                                  const int32_t* list, int64_t count, int force, int cap,
+                                  unsigned char* ws, size_t ws_bytes, int64_t ws_blocks,
+                                  int32_t* ovf_count, int32_t* ovf_list, hipStream_t stream) {
+  if (count <= 0) return hipSuccess;
+  int64_t grid;
+  if (CAP > 0) {
+    int occ = 0;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_ingest<CAP, VPL>, 64, 0);
+    if (occ <= 0) occ = 1;
+    grid = (int64_t)num_cu() * occ * 4;
+  } else {
+    grid = ws_blocks;
+  }
+  if (grid > count) grid = count;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL((k_ingest<CAP, VPL>), dim3((unsigned)grid), dim3(64), 0, stream, st, x, offs, list,
+                     count, force, cap, ws, ws_bytes, ovf_count, ovf_list);
+  return hipGetLastError();
+}
+
+template <int CAP>
+static hipError_t launch_ingest_vpl(int vpl, const GKState& st, const double* x, const int64_t* offs,
+                                    const int32_t* list, int64_t count, int force, int cap, unsigned char* ws,
+                                    size_t ws_bytes, int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list,
+                                    hipStream_t stream) {
+#define GK_L(V) launch_ingest_t<CAP, V>(st, x, offs, list, count, force, cap, ws, ws_bytes, ws_blocks, \
+                                        ovf_count, ovf_list, stream)
+  switch (vpl) {
+    case 1: return GK_L(1);
+    case 2: return GK_L(2);
+    case 4: return GK_L(4);
+    case 8: return GK_L(8);
+    case 16: return GK_L(16);
+    default: return hipErrorInvalidValue;
+  }
+#undef GK_L
+}
+
+size_t gk_ingest_ws_bytes(int cap, int vpl) { return gk_flush_ws_bytes(cap, vpl); }
+
+hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x, const int64_t* offs,
+                            const int32_t* list, int64_t count, int force, unsigned char* ws, size_t ws_bytes,
+                            int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list, hipStream_t stream) {
+  switch (cap) {
+    case 256:
+      return launch_ingest_vpl<256>(vpl, st, x, offs, list, count, force, cap, nullptr, 0, 0, ovf_count, ovf_list,
+                                    stream);
+    case 2048:
+      return launch_ingest_vpl<2048>(vpl, st, x, offs, list, count, force, cap, nullptr, 0, 0, ovf_count, ovf_list,
+                                     stream);
+    default:
+      if (!ws || ws_blocks <= 0) return hipErrorInvalidValue;
+      return launch_ingest_vpl<0>(vpl, st, x, offs, list, count, force, cap, ws, ws_bytes, ws_blocks, ovf_count,
+                                  ovf_list, stream);
+  }
+}
+
+hipError_t gk_launch_stats(const GKState& st, const double* x, const int64_t* offs, hipStream_t stream) {
+  if (st.S <= 0) return hipSuccess;
+  const int64_t grid = (st.S + 255) / 256;
+  hipLaunchKernelGGL(k_stats, dim3((unsigned)grid), dim3(256), 0, stream, st, x, offs);
+  return hipGetLastError();
+}
+
+hipError_t gk_launch_quantiles(const GKState& st, const double* qs, int nq, double* out, int mode,
+                               hipStream_t stream) {
+  if (st.S <= 0) return hipSuccess;
+  int64_t grid = (int64_t)num_cu() * 32;
+  if (grid > st.S) grid = st.S;
+  hipLaunchKernelGGL(k_quantiles, dim3((unsigned)grid), dim3(64), 0, stream, st, qs, nq, out, mode);
+  return hipGetLastError();
+}
+
+size_t gk_merge_lds_bytes(int cap, int pmax) {
+  const size_t MR = (size_t)cap + 1, MI = (size_t)cap + 1 + pmax;
+  size_t b = 8 * ((size_t)cap + MR + pmax + MI + cap) + 4 * (2 * (size_t)cap + 2 * MR + 2 * MI + 2 * (size_t)cap) + 16;
+  return (b + 255) & ~(size_t)255;
+}
+
+hipError_t gk_launch_merge(const MergeArgsHost& h, hipStream_t stream) {
+  if (h.count <= 0) return hipSuccess;
+  MergeArgs a;
+  a.dst = h.dst;
+  a.src = h.src;
+  a.ev = h.ev;
+  a.eg = h.eg;
+  a.ed = h.ed;
+  a.eoffs = h.eoffs;
+  a.mode = h.mode;
+  a.cap = h.cap;
+  a.list = h.list;
+  a.count = h.count;
+  a.ovf_count = h.ovf_count;
+  a.ovf_list = h.ovf_list;
+  a.ws = h.ws;
+  a.ws_bytes = h.ws_bytes;
+  const size_t lds = gk_merge_lds_bytes(h.cap, h.dst.pmax);
+  if (h.ws) {
+    if (h.ws_bytes < lds || h.ws_blocks <= 0) return hipErrorInvalidValue;
+    int64_t grid = h.ws_blocks;
+    if (grid > h.count) grid = h.count;
+    hipLaunchKernelGGL(k_merge<true>, dim3((unsigned)grid), dim3(64), 0, stream, a);
+    return hipGetLastError();
+  }
+  if (lds > 160 * 1024 - 64) return hipErrorInvalidValue;
+  if (lds > 48 * 1024)
+    (void)hipFuncSetAttribute((const void*)k_merge<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  int64_t grid = (int64_t)num_cu() * 8;
+  if (grid > h.count) grid = h.count;
+  hipLaunchKernelGGL(k_merge<false>, dim3((unsigned)grid), dim3(64), lds, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t gk_launch_reset(const GKState& st, hipStream_t stream) {
+  if (st.S <= 0) return hipSuccess;
+  const int64_t grid = (st.S + 255) / 256;
+  hipLaunchKernelGGL(k_reset, dim3((unsigned)grid), dim3(256), 0, stream, st);
+  return hipGetLastError();
+}
+
+static int64_t wave_grid(int64_t S) {
+  int64_t g = (S + 3) / 4;
+  const int64_t cap = (int64_t)num_cu() * 16;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return g;
+}
+
+hipError_t gk_launch_export(const GKState& st, const int64_t* offs, double* v, int32_t* g, int32_t* d,
+                            hipStream_t stream) {
+  if (st.S <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_export, dim3((unsigned)wave_grid(st.S)), dim3(256), 0, stream, st, offs, v, g, d);
+  return hipGetLastError();
+}
+
+hipError_t gk_launch_export_pending(const GKState& st, const int64_t* offs, double* v, hipStream_t stream) {
+  if (st.S <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_export_pending, dim3((unsigned)wave_grid(st.S)), dim3(256), 0, stream, st, offs, v);
+  return hipGetLastError();
+}
+
+hipError_t gk_launch_import(const GKState& st, const int64_t* offs, const double* v, const int32_t* g,
+                            const int32_t* d, const int64_t* poffs, const double* pv, int32_t* ovf_count,
+                            int32_t* ovf_list, hipStream_t stream) {
+  if (st.S <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_import, dim3((unsigned)wave_grid(st.S)), dim3(256), 0, stream, st, offs, v, g, d,
+                     poffs, pv, ovf_count, ovf_list);
+  return hipGetLastError();
+}
+
+hipError_t gk_launch_promote(const GKState& st, const int32_t* list, int64_t count, const int32_t* slots, int ncls,
+                             hipStream_t stream) {
+  if (count <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_promote, dim3((unsigned)wave_grid(count)), dim3(256), 0, stream, st, list, count, slots,
+                     ncls);
+  return hipGetLastError();
+}

@@ -1,0 +1,47 @@
+// gk_launch.h -- host-side launchers of the HIP kernels (gk_kernels.hip),
+// used by the C ABI runtime (gk_capi.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "gk_state.h"
+
+struct MergeArgsHost {
+  GKState dst;
+  GKState src;
+  const double* ev;
+  const int32_t* eg;
+  const int32_t* ed;
+  const int64_t* eoffs;
+  int mode;  // 0 = merge(other), 1 = merge_compress(entries)
+  int cap;
+  const int32_t* list;
+  int64_t count;
+  int32_t* ovf_count;
+  int32_t* ovf_list;
+  unsigned char* ws;  // global workspace for capacities beyond LDS (NULL = LDS)
+  size_t ws_bytes;    // per block
+  int64_t ws_blocks;
+};
+
+int gk_num_cu();
+size_t gk_ingest_ws_bytes(int cap, int vpl);
+// cap 256 / 2048: LDS kernels; any other cap: global workspace ws (ws_bytes per block, ws_blocks blocks)
+hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x, const int64_t* offs,
+                            const int32_t* list, int64_t count, int force, unsigned char* ws, size_t ws_bytes,
+                            int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list, hipStream_t stream);
+hipError_t gk_launch_stats(const GKState& st, const double* x, const int64_t* offs, hipStream_t stream);
+hipError_t gk_launch_quantiles(const GKState& st, const double* qs, int nq, double* out, int mode,
+                               hipStream_t stream);
+size_t gk_merge_lds_bytes(int cap, int pmax);
+hipError_t gk_launch_merge(const MergeArgsHost& h, hipStream_t stream);
+hipError_t gk_launch_reset(const GKState& st, hipStream_t stream);
+hipError_t gk_launch_export(const GKState& st, const int64_t* offs, double* v, int32_t* g, int32_t* d,
+                            hipStream_t stream);
+hipError_t gk_launch_export_pending(const GKState& st, const int64_t* offs, double* v, hipStream_t stream);
+hipError_t gk_launch_import(const GKState& st, const int64_t* offs, const double* v, const int32_t* g,
+                            const int32_t* d, const int64_t* poffs, const double* pv, int32_t* ovf_count,
+                            int32_t* ovf_list, hipStream_t stream);
+hipError_t gk_launch_promote(const GKState& st, const int32_t* list, int64_t count, const int32_t* slots, int ncls,
+                             hipStream_t stream);

@@ -1,0 +1,48 @@
+// gk_state.h -- device-side layout of a set of GKArray streams (shared by the
+// HIP kernels and the host runtime).  See DESIGN.md "Data layout in HBM".
+#pragma once
+#include <stdint.h>
+
+// One GK tuple (gk:8-16): value, g, delta.  16 bytes, so a wave moves 64
+// records (1 KiB) per coalesced dwordx4 access.
+struct GKRec {
+  double v;
+  int32_t g;
+  int32_t d;
+};
+
+#define GK_MAX_CLASSES 3
+
+// Per-set device pointers, passed by value to every kernel.
+struct GKState {
+  int64_t S;        // number of streams
+  double eps;       // gk:22
+  double two_eps;   // 2.0*eps, the first product of gk:70
+  double inv_eps;   // 1.0/eps, the small-n cutoff of gk:169 / gk:200
+  int32_t P;        // flush period int(1.0/eps)+1 (gk:60)
+  int32_t pmax;     // pending slots per stream (== P)
+
+  // header, structure of arrays [S]
+  int64_t* n;       // _n
+  int32_t* E;       // len(entries)
+  int32_t* pend;    // len(incoming)
+  double* mn;       // _min
+  double* mx;       // _max
+  double* sum;      // _sum
+  double* avg;      // _avg
+
+  // tables by capacity class: class 0 = tab[0] + s*cap[0] (every stream has
+  // one); class c > 0 = tab[c] + slot[s]*cap[c] for promoted streams.
+  int32_t* cls;     // capacity class of stream s
+  int32_t* slot;    // slot of stream s inside its class arena
+  GKRec* tab[GK_MAX_CLASSES];
+  int32_t cap[GK_MAX_CLASSES];
+  int32_t nclass;
+
+  double* pbuf;     // pending values: pbuf + s*pmax, insertion order
+};
+
+__host__ __device__ inline GKRec* gk_table_ptr(const GKState& st, int64_t s) {
+  const int32_t c = st.cls[s];
+  return c == 0 ? st.tab[0] + s * (int64_t)st.cap[0] : st.tab[c] + (int64_t)st.slot[s] * st.cap[c];
+}

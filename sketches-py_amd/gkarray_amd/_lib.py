@@ -1,0 +1,104 @@
+"""ctypes binding of the C ABI declared in ``include/gk_capi.h``.
+
+The shared library ``libgkarray_hip.so`` (built in-tree by ``make -C
+sketches-py_amd/csrc`` / ``__graft_entry__.build()``) holds every HIP kernel.
+There is no CPU fallback: if the library or a GPU is missing, the product path
+raises ``GKBackendError``.
+"""
+import ctypes
+import os
+
+__all__ = ["lib", "load", "GKBackendError", "check", "LIB_PATH", "SYMBOLS",
+           "GK_OK", "GK_E_ARG", "GK_E_EPS_MISMATCH", "GK_E_OVERFLOW", "GK_E_HIP",
+           "GK_E_NOMEM", "GK_E_UNSUPPORTED", "GK_Q_LIST", "GK_Q_SINGLE"]
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgkarray_hip.so")
+
+GK_OK = 0
+GK_E_ARG = -1
+GK_E_EPS_MISMATCH = -2
+GK_E_OVERFLOW = -3
+GK_E_HIP = -4
+GK_E_NOMEM = -5
+GK_E_UNSUPPORTED = -6
+GK_Q_LIST = 0
+GK_Q_SINGLE = 1
+
+
+class GKBackendError(RuntimeError):
+    """The HIP backend is missing or failed (no silent CPU fallback)."""
+
+    def __init__(self, code, msg):
+        super().__init__("gkarray_amd: %s (code %d)" % (msg, code))
+        self.code = code
+
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_I32 = ctypes.c_int32
+_D = ctypes.c_double
+_INT = ctypes.c_int
+
+# name -> (restype, argtypes); must match include/gk_capi.h exactly
+SYMBOLS = {
+    "gk_version": (_INT, []),
+    "gk_last_error": (ctypes.c_char_p, []),
+    "gk_create": (_INT, [_I64, _D, _I64, _INT, ctypes.POINTER(_P)]),
+    "gk_destroy": (_INT, [_P]),
+    "gk_reset": (_INT, [_P, _P]),
+    "gk_ingest": (_INT, [_P, _P, _P, _P]),
+    "gk_flush": (_INT, [_P, _P]),
+    "gk_quantiles": (_INT, [_P, ctypes.POINTER(_D), _INT, _P, _INT, _P]),
+    "gk_stats": (_INT, [_P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "gk_merge": (_INT, [_P, ctypes.POINTER(_P), _INT, _P]),
+    "gk_merge_compress": (_INT, [_P, _P, _P, _P, _P, _P]),
+    "gk_export_sizes": (_INT, [_P, _P, _P]),
+    "gk_export": (_INT, [_P, _P, _P, _P, _P, _P]),
+    "gk_export_pending_sizes": (_INT, [_P, _P, _P]),
+    "gk_export_pending": (_INT, [_P, _P, _P, _P]),
+    "gk_import": (_INT, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "gk_num_streams": (_I64, [_P]),
+    "gk_eps": (_D, [_P]),
+    "gk_flush_period": (_INT, [_P]),
+    "gk_capacity": (_INT, [_P, _INT]),
+    "gk_num_promoted": (_I64, [_P]),
+    "gk_timing_enable": (_INT, [_P, _INT]),
+    "gk_timing_read": (_INT, [_P, ctypes.POINTER(_D), ctypes.POINTER(_D), ctypes.POINTER(_I64)]),
+}
+
+_lib = None
+
+
+def load(path=None):
+    """Load the HIP library (cached).  Raises GKBackendError if it is absent."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise GKBackendError(GK_E_HIP, "HIP library not built: %s (run __graft_entry__.build())" % p)
+    try:
+        handle = ctypes.CDLL(p)
+    except OSError as e:  # pragma: no cover - depends on the ROCm install
+        raise GKBackendError(GK_E_HIP, "cannot load %s: %s" % (p, e))
+    for name, (res, args) in SYMBOLS.items():
+        fn = getattr(handle, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = handle
+    return handle
+
+
+def lib():
+    return load()
+
+
+def last_error():
+    return load().gk_last_error().decode("utf-8", "replace")
+
+
+def check(rc):
+    if rc != GK_OK:
+        raise GKBackendError(rc, last_error())
+    return rc

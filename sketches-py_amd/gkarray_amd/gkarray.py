@@ -1,0 +1,214 @@
+"""Drop-in ``GKArray`` backed by the MI355X engine.
+
+Mirrors ``gkarray/gkarray.py`` of githomin/sketches-py (``gk:N``): the same
+class names (``Entry``, ``GKArray``, ``UnequalEpsilonException``), method
+names, argument meaning, return values and errors.  Raw numbers may be passed
+to ``add`` directly (the reference evidently intends ``Entry(val, 1, 0)`` for
+them).
+
+``add`` appends to a host-side buffer; the buffer is shipped to the GPU in one
+``StreamSet.ingest`` call whenever state is observed (``_n``, ``entries``,
+``quantile`` ...) or it reaches ``GKArray.SHIP_CHUNK`` values.  Because flush
+points depend only on the running count ``n`` (gk:60), batching the adds does
+not change any result.  One GKArray = a StreamSet of one stream: use
+``StreamSet`` directly to sketch many streams at once.
+"""
+import math
+
+import numpy as np
+import torch
+
+from .streamset import StreamSet
+
+__all__ = ["Entry", "GKArray", "UnequalEpsilonException"]
+
+
+class UnequalEpsilonException(Exception):
+    """gk:4-5: raised by merge() when the two eps differ (gk:118-119)."""
+
+
+class Entry:
+    """gk:8-16 -- one (val, g, delta) record."""
+
+    def __init__(self, val, g, delta):
+        self.val = val
+        self.g = g
+        self.delta = delta
+
+    def __repr__(self):
+        return 'Entry(val={}, g={}, delta={})'.format(self.val, self.g, self.delta)
+
+
+def _is_nan(q):
+    try:
+        return q != q
+    except Exception:
+        return False
+
+
+class GKArray:
+    SHIP_CHUNK = 1 << 20
+
+    def __init__(self, eps, device=None):
+        # gk:21-29
+        self.eps = eps
+        self._set = StreamSet(1, eps, device)
+        self._buf = []
+        self._offs = None
+
+    # ---------------------------------------------------------------- plumbing
+    def _ship(self):
+        if self._buf:
+            vals = torch.tensor(self._buf, dtype=torch.float64, device=self._set.device)
+            offs = torch.tensor([0, len(self._buf)], dtype=torch.int64, device=self._set.device)
+            self._buf = []
+            self._set.ingest(vals, offs)
+
+    def _stats(self):
+        self._ship()
+        st = self._set.stats()
+        return {k: v[0].item() for k, v in st.items()}
+
+    @property
+    def name(self):
+        return 'GKArray'  # gk:31-33
+
+    # reference attributes, read-only views of the device state
+    @property
+    def _n(self):
+        return int(self._stats()["n"])
+
+    @property
+    def _min(self):
+        return float(self._stats()["min"])
+
+    @property
+    def _max(self):
+        return float(self._stats()["max"])
+
+    @property
+    def _sum(self):
+        return float(self._stats()["sum"])
+
+    @property
+    def _avg(self):
+        return float(self._stats()["avg"])
+
+    # convenience aliases named by the north star (eps is a plain attribute)
+    @property
+    def count(self):
+        return self._n
+
+    @property
+    def min(self):
+        return self._min
+
+    @property
+    def max(self):
+        return self._max
+
+    @property
+    def entries(self):
+        """Materialised copy of the table (gk:23); does not flush."""
+        self._ship()
+        return [Entry(v, g, d) for (v, g, d) in self._set.table(0)]
+
+    @property
+    def incoming(self):
+        """Pending raw values (gk:24), insertion order; does not flush."""
+        self._ship()
+        offs, pv = self._set.pending()
+        return pv.cpu().tolist()
+
+    # ---------------------------------------------------------------- accessors
+    def num_values(self):
+        return self._n  # gk:35-36
+
+    def avg(self):
+        return self._avg  # gk:38-39
+
+    def sum(self):
+        return self._sum  # gk:41-42
+
+    def size(self):
+        # gk:44-47: flush pending values, then the table length
+        self._ship()
+        self._set.flush()
+        return int(self._set.stats()["size"][0].item())
+
+    # ---------------------------------------------------------------- ingest
+    def add(self, val):
+        """gk:49-61 (buffered; flush points are decided on the GPU)."""
+        self._buf.append(float(val))
+        if len(self._buf) >= self.SHIP_CHUNK:
+            self._ship()
+
+    def add_many(self, values):
+        """Extension: ``for v in values: add(v)`` in one call."""
+        self._ship()
+        t = torch.as_tensor(values, dtype=torch.float64).reshape(-1)
+        if t.numel():
+            self._set.ingest(t.to(self._set.device),
+                             torch.tensor([0, t.numel()], dtype=torch.int64, device=self._set.device))
+
+    def merge_compress(self, entries=[]):
+        """gk:63-109.  With entries, they are merged as records (v, g, delta)."""
+        self._ship()
+        if not entries:
+            self._set.merge_compress()
+            return
+        recs = [(float(e.val), int(e.g), int(e.delta)) for e in entries]
+        # sorted() in gk:72 is stable: records of equal value keep their order
+        recs = sorted(recs, key=lambda r: r[0])
+        v = torch.tensor([r[0] for r in recs], dtype=torch.float64)
+        g = torch.tensor([r[1] for r in recs], dtype=torch.int32)
+        d = torch.tensor([r[2] for r in recs], dtype=torch.int32)
+        self._set.merge_compress(v, g, d, torch.tensor([0, len(recs)], dtype=torch.int64))
+
+    # ---------------------------------------------------------------- merge
+    def merge(self, other):
+        """gk:111-154 (flushes `other`, like the reference)."""
+        if self.eps != other.eps:
+            raise UnequalEpsilonException("Cannot merge two GKArrays with different epsilon values")
+        self._ship()
+        other._ship()
+        self._set.merge_from([other._set])
+        self.eps = max(self.eps, other.eps)
+
+    # ---------------------------------------------------------------- query
+    def quantile(self, q):
+        """gk:156-185."""
+        if q < 0 or q > 1:
+            return np.nan
+        st = self._stats()
+        if st["n"] == 0:
+            return np.nan
+        if _is_nan(q):
+            self._set.flush()
+            raise ValueError("cannot convert float NaN to integer")
+        out = self._set.quantiles([q], single=True)
+        return np.float64(out[0, 0].item())
+
+    def quantiles(self, q_values):
+        """gk:187-232."""
+        st = self._stats()
+        if st["n"] == 0:
+            return [np.nan] * len(q_values)
+        self._set.flush()
+        small = st["n"] < 1.0 / self.eps
+        qs = list(q_values)
+        nan_pos = [k for k, q in enumerate(qs) if _is_nan(q)]
+        if small:
+            safe = [(-1.0 if _is_nan(q) else float(q)) for q in qs]
+            out = self._set.quantiles(safe, single=True)[0].cpu().tolist() if qs else []
+            return [np.nan if k in nan_pos else np.float64(v) for k, v in enumerate(out)]
+        if isinstance(q_values, np.ndarray):
+            # gk:205: `ndarray != list` is an array; its truth value raises
+            raise ValueError("The truth value of an array with more than one element is ambiguous. "
+                             "Use a.any() or a.all()")
+        if nan_pos:
+            raise ValueError("cannot convert float NaN to integer")
+        # gk:205: a tuple never equals sorted(...) (a list) -> per-q quantile()
+        single = (not isinstance(q_values, list)) or (qs != sorted(qs))
+        out = self._set.quantiles([float(q) for q in qs], single=single)[0].cpu().tolist()
+        return [np.nan if math.isnan(v) else v for v in out]

@@ -1,0 +1,359 @@
+"""Parity of the HIP path (through the C ABI) with the reference.
+
+* against the golden vectors produced by the reference itself
+  (tests/golden/make_golden.py) -- every stream, mid-stream query and merge
+  case, batched into StreamSets;
+* against the C restatement of the oracle (pinned by test_oracle_golden.py) on
+  seeded random batches, with random chunking of the ingest calls;
+* size-independent properties at larger sizes.
+
+Bar: bit-exact tables (v, g, delta), pending values, n/min/max/sum/avg and
+quantiles.  One documented tolerance: the sign of a zero from the small-n
+numpy.percentile branch (see test_oracle_golden.py).
+"""
+import numpy as np
+import pytest
+import torch
+
+import golden_io as G
+from gk_oracle_c import OracleSet
+
+pytestmark = pytest.mark.gpu
+
+
+def _ss(S, eps, dev, **kw):
+    from gkarray_amd import StreamSet
+    return StreamSet(S, eps, device=dev, **kw)
+
+
+def same_q(a, b):
+    return G.same_float(a, b) or (a == 0 and b == 0)
+
+
+def csr(seqs):
+    offs = np.zeros(len(seqs) + 1, np.int64)
+    offs[1:] = np.cumsum([len(x) for x in seqs])
+    flat = np.concatenate([np.asarray(x, np.float64) for x in seqs]) if len(seqs) else np.zeros(0)
+    return flat, offs
+
+
+def ingest_np(ss, seqs):
+    flat, offs = csr(seqs)
+    ss.ingest(torch.from_numpy(flat), torch.from_numpy(offs))
+
+
+def tables_np(ss):
+    offs, v, g, d = ss.tables()
+    return offs.cpu().numpy(), v.cpu().numpy(), g.cpu().numpy(), d.cpu().numpy()
+
+
+def assert_same_tables(ss, osx, ids=None, what=""):
+    go, gv, gg, gd = tables_np(ss)
+    oo, ov, og, od = osx.tables()
+    S = ss.num_streams
+    ids = range(S) if ids is None else ids
+    for s in ids:
+        a, b = go[s], go[s + 1]
+        c, e = oo[s], oo[s + 1]
+        assert b - a == e - c, "%s stream %d: size %d vs %d" % (what, s, b - a, e - c)
+        assert np.array_equal(gv[a:b].view(np.int64), ov[c:e].view(np.int64)), "%s stream %d values" % (what, s)
+        assert np.array_equal(gg[a:b].astype(np.int64), og[c:e]), "%s stream %d g" % (what, s)
+        assert np.array_equal(gd[a:b].astype(np.int64), od[c:e]), "%s stream %d delta" % (what, s)
+
+
+def assert_same_state(ss, osx, what=""):
+    assert_same_tables(ss, osx, what=what)
+    gp_o, gp_v = ss.pending()
+    op_o, op_v = osx.pending()
+    assert np.array_equal(gp_o.cpu().numpy(), op_o), what + " pending offsets"
+    assert np.array_equal(gp_v.cpu().numpy().view(np.int64), op_v.view(np.int64)), what + " pending"
+    st = {k: v.cpu().numpy() for k, v in ss.stats().items()}
+    ost = osx.stats()
+    for k in ("n", "size", "pending"):
+        assert np.array_equal(st[k].astype(np.int64), ost[k].astype(np.int64)), what + " " + k
+    for k in ("min", "max", "sum", "avg"):
+        assert np.array_equal(st[k].view(np.int64), ost[k].view(np.int64)), what + " " + k
+
+
+def assert_same_quantiles(got, exp, what=""):
+    got = np.asarray(got)
+    exp = np.asarray(exp)
+    assert got.shape == exp.shape
+    bad = [(i, got.flat[i], exp.flat[i]) for i in range(got.size) if not same_q(got.flat[i], exp.flat[i])]
+    assert not bad, "%s: %d mismatches, first %r" % (what, len(bad), bad[:3])
+
+
+# ----------------------------------------------------------------------------
+# golden vectors from the reference
+# ----------------------------------------------------------------------------
+def test_golden_streams(gpu_device):
+    by_eps = {}
+    for c in G.cases("stream"):
+        by_eps.setdefault(c["eps"], []).append(c)
+    for eps, cs in by_eps.items():
+        ss = _ss(len(cs), eps, gpu_device)
+        ingest_np(ss, [G.get(c["id"], "x") for c in cs])
+        for k, c in enumerate(cs):
+            assert G.same_table(ss.table(k), G.tables(c["id"], "auto")[0]), c
+        poffs, pv = ss.pending()
+        poffs, pv = poffs.cpu().numpy(), pv.cpu().numpy()
+        st = {k: v.cpu().numpy() for k, v in ss.stats().items()}
+        for k, c in enumerate(cs):
+            assert np.array_equal(pv[poffs[k]:poffs[k + 1]].view(np.int64),
+                                  G.get(c["id"], "pending").view(np.int64)), c
+            got = [st["n"][k], st["min"][k], st["max"][k], st["sum"][k], st["avg"][k]]
+            assert all(G.same_float(a, b) for a, b in zip(got, G.get(c["id"], "stats_before_query"))), c
+        q = ss.quantiles(G.index()["qs"], single=True).cpu().numpy()
+        for k, c in enumerate(cs):
+            assert_same_quantiles(q[k], G.get(c["id"], "q_single"), "quantile %r" % c)
+            assert G.same_table(ss.table(k), G.tables(c["id"], "final")[0]), c
+        q = ss.quantiles(G.index()["qs"]).cpu().numpy()
+        q2 = ss.quantiles(G.index()["qs_unsorted"]).cpu().numpy()
+        q3 = ss.quantiles(G.index()["qs_oor"]).cpu().numpy()
+        for k, c in enumerate(cs):
+            assert_same_quantiles(q[k], G.get(c["id"], "q_sorted"), "quantiles %r" % c)
+            assert_same_quantiles(q2[k], G.get(c["id"], "q_unsorted"), "unsorted %r" % c)
+            assert_same_quantiles(q3[k], G.get(c["id"], "q_oor"), "oor %r" % c)
+        st = ss.stats()
+        for k, c in enumerate(cs):
+            assert int(st["size"][k]) == int(G.get(c["id"], "size")[0])
+
+
+def test_golden_query_mid(gpu_device):
+    for c in G.cases("query_mid"):
+        cid, eps = c["id"], c["eps"]
+        xs = G.get(cid, "x")
+        pts = [int(p) for p in G.get(cid, "query_points")]
+        exp_q = G.get(cid, "mid_q")
+        exp_t = G.tables(cid, "mid_tables")
+        ss = _ss(1, eps, gpu_device)
+        prev = 0
+        for k, p in enumerate(pts):
+            ingest_np(ss, [xs[prev:p]])
+            assert_same_quantiles(ss.quantiles([0.1, 0.5, 0.9]).cpu().numpy()[0], exp_q[k], "mid %r" % c)
+            assert G.same_table(ss.table(0), exp_t[k]), c
+            prev = p
+        ingest_np(ss, [xs[prev:]])
+        assert G.same_table(ss.table(0), exp_t[-1]), c
+
+
+def test_golden_merges(gpu_device):
+    for c in G.cases("merge"):
+        cid, eps = c["id"], c["eps"]
+        shards = G.shards(cid)
+        sets = []
+        for xs in shards:
+            ss = _ss(1, eps, gpu_device)
+            ingest_np(ss, [xs])
+            sets.append(ss)
+        steps = G.tables(cid, "merge_steps")
+        others = G.tables(cid, "others_after")
+        acc = sets[0]
+        for k, o in enumerate(sets[1:]):
+            acc.merge_from([o])
+            assert G.same_table(acc.table(0), steps[k]), (c, k)
+            assert G.same_table(o.table(0), others[k]), (c, k)
+        st = {k: v.cpu().numpy() for k, v in acc.stats().items()}
+        got = [st["n"][0], st["min"][0], st["max"][0], st["sum"][0], st["avg"][0]]
+        assert all(G.same_float(a, b) for a, b in zip(got, G.get(cid, "merged_stats"))), c
+        assert_same_quantiles(acc.quantiles(G.index()["qs"]).cpu().numpy()[0], G.get(cid, "merged_q"), c)
+
+
+def test_eps_mismatch(gpu_device):
+    from gkarray_amd import UnequalEpsilonException
+    a = _ss(4, 0.01, gpu_device)
+    b = _ss(4, 0.02, gpu_device)
+    with pytest.raises(UnequalEpsilonException):
+        a.merge_from([b])
+
+
+def test_drop_in_gkarray_kat(gpu_device):
+    from gkarray_amd import GKArray, UnequalEpsilonException
+    kat = G.index()["kat"]
+    sk = GKArray(0.1)
+    xs = [float((7 * i) % 23) for i in range(40)]
+    for x in xs[:33]:
+        sk.add(x)
+    assert [(e.val, e.g, e.delta) for e in sk.entries] == [tuple(r) for r in kat["kat1_table_after_33"]]
+    for x in xs[33:]:
+        sk.add(x)
+    assert sk.quantiles([0, .25, .5, .75, 1]) == [0, 5, 10, 19, 22]
+    assert [(e.val, e.g, e.delta) for e in sk.entries] == [tuple(r) for r in kat["kat1_final_table"]]
+    sk = GKArray(0.1)
+    for x in [3.0, 1.0, 2.0]:
+        sk.add(x)
+    assert sk.quantile(.5) == 2.0 and sk.quantile(.25) == 1.5
+    assert sk.num_values() == 3 and sk.name == "GKArray"
+    assert np.isnan(sk.quantile(1.5)) and np.isnan(sk.quantile(-0.1))
+    e = GKArray(0.1)
+    assert np.isnan(e.quantile(0.5)) and all(np.isnan(v) for v in e.quantiles([0.1, 0.2]))
+    with pytest.raises(UnequalEpsilonException):
+        sk.merge(GKArray(0.2))
+    big = GKArray(0.01)
+    big.add_many(np.random.default_rng(0).random(1_000_000))
+    assert big.quantiles([.5, .9, .99]) == kat["kat3_quantiles"]
+    assert big.size() == kat["kat3_size"]
+    st = kat["kat3_stats"]
+    assert [big._n, big._min, big._max, big._sum, big._avg] == st
+
+
+# ----------------------------------------------------------------------------
+# random batches against the C oracle
+# ----------------------------------------------------------------------------
+def gen(dist, L, rng):
+    if dist == 0:
+        return rng.random(L)
+    if dist == 1:
+        return rng.lognormal(0, 1, L)
+    if dist == 2:
+        return rng.pareto(1.5, L) + 1
+    if dist == 3:
+        return np.sort(rng.random(L))[::-1].copy()
+    if dist == 4:
+        return np.sort(rng.random(L))
+    if dist == 5:
+        return rng.integers(0, 5, L).astype(np.float64)
+    if dist == 6:
+        return rng.choice(np.array([0.0, -0.0, 1.0, -1.0]), L)
+    return np.round(rng.normal(0, 2, L), 1)
+
+
+@pytest.mark.parametrize("eps", [0.2, 0.1, 0.05, 0.03, 0.015, 0.01, 0.001])
+def test_random_batches_vs_oracle(gpu_device, eps):
+    rng = np.random.default_rng(int(eps * 1e6) + 11)
+    S = 600 if eps >= 0.01 else 120
+    P = int(1.0 / eps) + 1
+    lens = rng.integers(0, 12 * P, S)
+    lens[:4] = [0, 1, P, P - 1]
+    dists = rng.integers(0, 8, S)
+    seqs = [gen(int(d), int(L), rng) for d, L in zip(dists, lens)]
+    ss = _ss(S, eps, gpu_device)
+    osx = OracleSet(S, eps)
+    # ingest in 3 random chunks per stream (different split points per stream)
+    cuts = [np.sort(rng.integers(0, max(len(x), 1) + 1, 2)) for x in seqs]
+    for part in range(3):
+        piece = []
+        for x, c in zip(seqs, cuts):
+            a = 0 if part == 0 else int(c[part - 1])
+            b = int(c[part]) if part < 2 else len(x)
+            piece.append(x[a:b])
+        flat, offs = csr(piece)
+        ss.ingest(torch.from_numpy(flat), torch.from_numpy(offs))
+        osx.ingest(flat, offs)
+        assert_same_state(ss, osx, "eps=%g part %d" % (eps, part))
+    for qs, single in (([0.5, 0.9, 0.99], False), ([0.99, 0.1, 0.5], False),
+                       ([0.0, 0.25, 1.0, 1.2, -0.3], True)):
+        got = ss.quantiles(qs, single=single).cpu().numpy()
+        exp = osx.quantiles(qs, single=single)
+        assert_same_quantiles(got, exp, "eps=%g qs=%r" % (eps, qs))
+    assert_same_state(ss, osx, "after queries")
+
+
+def test_overflow_promotion(gpu_device):
+    """Descending streams outgrow the 256-entry fast class and are promoted."""
+    rng = np.random.default_rng(5)
+    S = 40
+    seqs = [np.sort(rng.random(int(L)))[::-1].copy() for L in rng.integers(20000, 60000, S)]
+    seqs[0] = rng.random(3000)
+    ss = _ss(S, 0.01, gpu_device)
+    osx = OracleSet(S, 0.01)
+    flat, offs = csr(seqs)
+    ss.ingest(torch.from_numpy(flat), torch.from_numpy(offs))
+    osx.ingest(flat, offs)
+    assert ss.num_promoted > 0
+    assert_same_state(ss, osx, "promoted")
+    got = ss.quantiles([0.01, 0.5, 0.99]).cpu().numpy()
+    assert_same_quantiles(got, osx.quantiles([0.01, 0.5, 0.99]), "promoted q")
+    # keep ingesting after promotion
+    seqs2 = [rng.random(int(L)) for L in rng.integers(0, 3000, S)]
+    flat, offs = csr(seqs2)
+    ss.ingest(torch.from_numpy(flat), torch.from_numpy(offs))
+    osx.ingest(flat, offs)
+    assert_same_state(ss, osx, "after promotion")
+
+
+@pytest.mark.parametrize("eps", [0.1, 0.01])
+def test_merge_fold_vs_oracle(gpu_device, eps):
+    rng = np.random.default_rng(17)
+    S, K = 300, 8
+    P = int(1.0 / eps) + 1
+    gsets, osets = [], []
+    for k in range(K):
+        lens = rng.integers(0, 10 * P, S)
+        if k == 0:
+            lens[:10] = 0
+        seqs = [gen(int(d), int(L), rng) for d, L in zip(rng.integers(0, 8, S), lens)]
+        flat, offs = csr(seqs)
+        g = _ss(S, eps, gpu_device)
+        g.ingest(torch.from_numpy(flat), torch.from_numpy(offs))
+        o = OracleSet(S, eps)
+        o.ingest(flat, offs)
+        gsets.append(g)
+        osets.append(o)
+    gsets[0].merge_from(gsets[1:])
+    for o in osets[1:]:
+        osets[0].merge(o)
+    assert_same_state(gsets[0], osets[0], "fold")
+    for g, o in zip(gsets[1:], osets[1:]):
+        assert_same_tables(g, o, what="mutated source")
+    got = gsets[0].quantiles([0.5, 0.9, 0.99]).cpu().numpy()
+    assert_same_quantiles(got, osets[0].quantiles([0.5, 0.9, 0.99]), "fold q")
+
+
+def test_export_import_roundtrip(gpu_device):
+    rng = np.random.default_rng(23)
+    S = 500
+    seqs = [rng.lognormal(0, 1, int(L)) for L in rng.integers(0, 3000, S)]
+    a = _ss(S, 0.01, gpu_device)
+    ingest_np(a, seqs)
+    state = a.export_state()
+    b = _ss(S, 0.01, gpu_device)
+    b.import_state(state)
+    more = [rng.random(int(L)) for L in rng.integers(0, 500, S)]
+    ingest_np(a, more)
+    ingest_np(b, more)
+    qa = a.quantiles([0.1, 0.5, 0.9]).cpu().numpy()
+    qb = b.quantiles([0.1, 0.5, 0.9]).cpu().numpy()
+    assert np.array_equal(qa.view(np.int64), qb.view(np.int64))
+    ta, tb = tables_np(a), tables_np(b)
+    for x, y in zip(ta, tb):
+        assert np.array_equal(x, y)
+
+
+def test_large_batch_properties_and_sample(gpu_device):
+    """cfg3-shaped batch (200k streams x 1000 Pareto values): size-independent
+    properties on every stream, exact parity on a 2,000-stream sample."""
+    S, L, eps = 200_000, 1000, 0.01
+    g = torch.Generator(device=gpu_device)
+    g.manual_seed(3)
+    u = torch.rand(S * L, dtype=torch.float64, device=gpu_device, generator=g)
+    x = (1.0 - u).pow(-1.0 / 1.5)  # Pareto(1.5) + 1
+    offs = torch.arange(0, S * L + 1, L, dtype=torch.int64, device=gpu_device)
+    ss = _ss(S, eps, gpu_device)
+    ss.ingest(x, offs)
+    st = ss.stats()
+    assert bool((st["n"] == L).all())
+    assert bool((st["pending"] == L % 101).all())
+    offs_t, v, gg, dd = ss.tables()
+    # sum of g == n - pending for add-only streams; table sorted by value
+    seg = torch.repeat_interleave(torch.arange(S, device=gpu_device), (offs_t[1:] - offs_t[:-1]))
+    gsum = torch.zeros(S, dtype=torch.int64, device=gpu_device).index_add_(0, seg, gg.to(torch.int64))
+    assert bool((gsum == L - L % 101).all())
+    same_seg = seg[1:] == seg[:-1]
+    assert bool((v[1:][same_seg] >= v[:-1][same_seg]).all())
+    q = ss.quantiles([0.5, 0.9, 0.99])
+    assert bool((q[:, 0] <= q[:, 1]).all()) and bool((q[:, 1] <= q[:, 2]).all())
+    # exact parity on a sample of streams
+    idx = np.random.default_rng(1).choice(S, 2000, replace=False)
+    xs = x.view(S, L)[torch.from_numpy(idx).to(gpu_device)].cpu().numpy()
+    o = OracleSet(len(idx), eps)
+    o.ingest(xs.reshape(-1), np.arange(0, len(idx) * L + 1, L))
+    oq = o.quantiles([0.5, 0.9, 0.99])
+    assert_same_quantiles(q.cpu().numpy()[idx], oq, "sample quantiles")
+    go, gv, ggn, gdn = offs_t.cpu().numpy(), v.cpu().numpy(), gg.cpu().numpy(), dd.cpu().numpy()
+    oo, ov, og, od = o.tables()
+    for k, s in enumerate(idx[:500]):
+        a, b = go[s], go[s + 1]
+        assert np.array_equal(gv[a:b].view(np.int64), ov[oo[k]:oo[k + 1]].view(np.int64))
+        assert np.array_equal(ggn[a:b].astype(np.int64), og[oo[k]:oo[k + 1]])
+        assert np.array_equal(gdn[a:b].astype(np.int64), od[oo[k]:oo[k + 1]])
