@@ -72,6 +72,7 @@ struct gk_set {
   // overflow reporting
   int32_t* d_ovf_count = nullptr;
   int32_t* d_ovf_list = nullptr;
+  int64_t* d_zero_offs = nullptr;  // S+1 zeros: offsets of flush-only launches
   // scratch
   double* d_qs = nullptr;
   int qs_alloc = 0;
@@ -218,17 +219,20 @@ hipError_t launch_class(gk_set* h, int c, const double* x, const int64_t* offs, 
 // larger class over its member list); streams that overflow their class were
 // not committed, so they are promoted one class up and run again.
 int run_ingest(gk_set* h, const double* x, const int64_t* offs, int force, hipStream_t stream) {
+  if (!offs) offs = h->d_zero_offs;
   HIP_TRY(hipMemsetAsync(h->d_ovf_count, 0, sizeof(int32_t), stream));
-  if (h->timing) HIP_TRY(hipEventRecord(h->ev[0], stream));
+  // timing covers the class-0 batch launch of gk_ingest (force == 0) only
+  const bool timed = h->timing && force == 0;
+  if (timed) HIP_TRY(hipEventRecord(h->ev[0], stream));
   HIP_TRY(launch_class(h, 0, x, offs, nullptr, h->S, force, stream));
-  if (h->timing) HIP_TRY(hipEventRecord(h->ev[1], stream));
+  if (timed) HIP_TRY(hipEventRecord(h->ev[1], stream));
   for (int c = 1; c < h->st.nclass; ++c)
     if (!h->members[c].empty())
       HIP_TRY(launch_class(h, c, x, offs, h->d_list[c], (int64_t)h->members[c].size(), force, stream));
   std::vector<int32_t> ovf;
   int64_t cnt = read_overflow(h, ovf, stream);
   if (cnt < 0) return (int)cnt;
-  if (h->timing) {
+  if (timed) {
     float ms = 0;
     HIP_TRY(hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
     h->flush_ms += ms;
@@ -375,6 +379,7 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
   okm &= hipMalloc(&st.pbuf, (size_t)S * st.pmax * sizeof(double)) == hipSuccess;
   okm &= hipMalloc(&h->d_ovf_count, sizeof(int32_t)) == hipSuccess;
   okm &= hipMalloc(&h->d_ovf_list, S * sizeof(int32_t)) == hipSuccess;
+  okm &= hipMalloc(&h->d_zero_offs, (S + 1) * sizeof(int64_t)) == hipSuccess;
   if (!okm) {
     gk_destroy(h);
     return fail(GK_E_NOMEM, "device allocation for %lld streams failed", (long long)num_streams);
@@ -385,6 +390,7 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
     return GK_E_NOMEM;
   }
   if (hipMemset(st.cls, 0, S * sizeof(int32_t)) != hipSuccess ||
+      hipMemset(h->d_zero_offs, 0, (S + 1) * sizeof(int64_t)) != hipSuccess ||
       hipMemset(st.slot, 0, S * sizeof(int32_t)) != hipSuccess || gk_launch_reset(st, nullptr) != hipSuccess ||
       hipDeviceSynchronize() != hipSuccess) {
     gk_destroy(h);
@@ -401,7 +407,7 @@ int gk_destroy(gk_set* h) {
   void* ptrs[] = {st.n,       st.E,           st.pend,          st.mn,          st.mx,         st.sum,
                   st.avg,     st.cls,         st.slot,          st.tab[0],      st.tab[1],     st.tab[2],
                   st.pbuf,    h->d_list[0],   h->d_list[1],     h->d_list[2],   h->d_qs,       h->d_ovf_count,
-                  h->d_ovf_list, h->d_tmp_list, h->d_tmp_slots, h->d_ws};
+                  h->d_ovf_list, h->d_tmp_list, h->d_tmp_slots, h->d_ws, h->d_zero_offs};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (auto& e : h->ev)

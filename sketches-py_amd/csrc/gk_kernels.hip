@@ -41,13 +41,28 @@ __device__ __forceinline__ int clampi(int x, int lo, int hi) { return x < lo ? l
 // ---------------------------------------------------------------------------
 // wave helpers (wave64)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v, int lane) {
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    uint32_t t = __shfl_up(v, o, 64);
-    if (lane >= o) v += t;
-  }
+// DPP controls (GFX9 family, gfx950 included)
+#define DPP_ROW_SHR(n) (0x110 + (n))
+#define DPP_WAVE_SHR1 0x138
+#define DPP_ROW_BCAST15 0x142
+#define DPP_ROW_BCAST31 0x143
+
+// Inclusive wave64 prefix sum in 12 VALU ops: Hillis-Steele inside each row
+// of 16 lanes, then the row_bcast15/31 carries across rows.  Lanes whose DPP
+// source is outside the row (or rows masked off) receive 0.
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v, int /*lane*/) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, DPP_ROW_SHR(1), 0xf, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, DPP_ROW_SHR(2), 0xf, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, DPP_ROW_SHR(4), 0xf, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, DPP_ROW_SHR(8), 0xf, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, DPP_ROW_BCAST15, 0xa, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, DPP_ROW_BCAST31, 0xc, 0xf, false);
   return v;
+}
+
+// value of lane-1 (lane 0 gets `fill`)
+__device__ __forceinline__ int wave_shr1(int v, int fill) {
+  return __builtin_amdgcn_update_dpp(fill, v, DPP_WAVE_SHR1, 0xf, 0xf, false);
 }
 
 __device__ __forceinline__ int64_t wave_incl_scan_i64(int64_t v, int lane) {
@@ -74,34 +89,139 @@ __device__ __forceinline__ int wave_sum_i32(int v) {
   return v;
 }
 
+// Ordering point for a ONE-WAVE workgroup.  The LDS executes a wave's
+// instructions in issue order, so a ds_write is visible to every later
+// ds_read of the same wave; only the compiler must not move LDS accesses
+// across this point.  Unlike __syncthreads() it does not wait for vmcnt, so
+// global-memory prefetches stay in flight.  The global-workspace variant
+// (GLOBAL = true) needs the memory counters drained and keeps __syncthreads.
+template <bool GLOBAL>
+__device__ __forceinline__ void wsync() {
+  if constexpr (GLOBAL) {
+    __syncthreads();
+  } else {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+
+// ---------------------------------------------------------------------------
+// Explicit prefetch.  hipcc's waitcnt pass is conservative across loop
+// iterations: a register loaded in iteration k and used in k+1 gets a
+// vmcnt(0) wait in front of its first use, which also waits for every load
+// issued since.  These loads are invisible to that pass; the consumer waits
+// with gk_vm_wait(), which ties the registers so no use moves above it.
+// (Correctness of the compiler's own counted waits is unaffected: loads retire
+// in order, so extra outstanding loads only make its vmcnt(N) stricter.)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void gk_load_async(double& dst, const double* p) {
+  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(dst) : "v"(p) : "memory");
+}
+
+template <int VPL>
+__device__ __forceinline__ void gk_vm_wait(double (&v)[VPL]) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int r = 0; r < VPL; ++r) asm volatile("" : "+v"(v[r]));
+}
+
+
+// A flush's values: the first p come from the stream's pending buffer, the
+// rest from the batch.  Loaded explicitly and waited for here, so that no
+// compiler-visible load is outstanding on these registers afterwards.
+template <int VPL>
+__device__ __forceinline__ void gk_load_flush_values(double (&xv)[VPL], const double* pb, int p,
+                                                     const double* xs, int cnt, int lane) {
+#pragma unroll
+  for (int r = 0; r < VPL; ++r) {
+    const int i = lane + 64 * r;
+    const int ic = min(i, max(cnt - 1, 0));
+    const double* a = (ic < p) ? pb + ic : xs + (ic - p);
+    if (cnt > 0) gk_load_async(xv[r], a);
+  }
+  if (cnt > 0) gk_vm_wait<VPL>(xv);
+#pragma unroll
+  for (int r = 0; r < VPL; ++r) xv[r] = (lane + 64 * r < cnt) ? xv[r] : 0.0;
+}
+
 // ===========================================================================
-// k_stats: gk:52-59 for every value, one lane per stream (the _sum/_avg
-// updates are a dependent float64 chain in insertion order, so a stream's
-// chain stays on one lane; 64 streams run side by side in a wave).
-// The header n is NOT written here: k_ingest owns n and runs after this
-// kernel on the same HIP stream, so both read the pre-call n.
+// k_stats: gk:52-59 for every value.  The _sum/_avg updates are a dependent
+// float64 chain in insertion order, so each stream's chain runs on one lane
+// (a 256-thread block = 256 streams).  The block stages its streams' values
+// through LDS in chunks of STATS_CHUNK values per stream: 16 lanes load one
+// stream's chunk as one contiguous 128-byte run (full HBM lines), then every
+// lane walks its own row.  The header n is NOT written here: k_ingest owns
+// n and runs after this kernel on the same HIP stream, so both read the
+// pre-call n.
 // ===========================================================================
+#define STATS_CHUNK 16
+#define STATS_ROW (STATS_CHUNK + 1)  // +1 double: lanes' rows start on different banks
+
 __global__ __launch_bounds__(256) void k_stats(GKState st, const double* __restrict__ x,
                                                const int64_t* __restrict__ offs) {
-  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= st.S) return;
-  const int64_t o = offs[s], L = offs[s + 1] - o;
-  if (L <= 0) return;
-  int64_t n = st.n[s];
-  double mn = st.mn[s], mx = st.mx[s], sm = st.sum[s], av = st.avg[s];
-  const double* p = x + o;
-  for (int64_t i = 0; i < L; ++i) {
-    const double v = p[i];
-    n += 1;                               // gk:52
-    sm = sm + v;                          // gk:53
-    av = av + (v - av) * (1.0 / (double)n);  // gk:54 (no FMA: -ffp-contract=off)
-    if (v < mn) mn = v;                   // gk:56-57 (strict: first occurrence kept)
-    if (v > mx) mx = v;                   // gk:58-59
+  __shared__ double tile[256 * STATS_ROW];
+  __shared__ int64_t so[257];
+  __shared__ int64_t smax;
+  const int t = threadIdx.x;
+  const int64_t s0 = (int64_t)blockIdx.x * 256;
+  const int nstr = (int)min((int64_t)256, st.S - s0);
+  if (t < nstr) so[t] = offs[s0 + t];
+  if (t == 0) {
+    so[nstr] = offs[s0 + nstr];
+    smax = 0;
   }
-  st.mn[s] = mn;
-  st.mx[s] = mx;
-  st.sum[s] = sm;
-  st.avg[s] = av;
+  __syncthreads();
+  int64_t L = 0;
+  if (t < nstr) L = so[t + 1] - so[t];
+  // block-uniform trip count: the longest stream of the block
+  atomicMax((unsigned long long*)&smax, (unsigned long long)L);
+  __syncthreads();
+  const int64_t maxL = smax;
+  if (maxL == 0) return;
+  const int64_t s = s0 + t;
+  int64_t n = 0;
+  double mn = 0, mx = 0, sm = 0, av = 0;
+  if (t < nstr) {
+    n = st.n[s];
+    mn = st.mn[s];
+    mx = st.mx[s];
+    sm = st.sum[s];
+    av = st.avg[s];
+  }
+  const int sub = t & 15;   // lane within a stream's 16-lane group
+  const int grp = t >> 4;   // 16 streams per pass
+  for (int64_t k0 = 0; k0 < maxL; k0 += STATS_CHUNK) {
+#pragma unroll 4
+    for (int r = 0; r < 16; ++r) {
+      const int ls = r * 16 + grp;
+      if (ls < nstr) {
+        const int64_t o = so[ls], e = so[ls + 1];
+        const int64_t i = o + k0 + sub;
+        tile[ls * STATS_ROW + sub] = (i < e) ? x[i] : 0.0;
+      }
+    }
+    __syncthreads();
+    if (t < nstr) {
+      const int kmax = (int)min((int64_t)STATS_CHUNK, L - k0);
+      for (int k = 0; k < kmax; ++k) {
+        const double v = tile[t * STATS_ROW + k];
+        n += 1;                                   // gk:52
+        sm = sm + v;                              // gk:53
+        av = av + (v - av) * (1.0 / (double)n);   // gk:54 (no FMA: -ffp-contract=off)
+        if (v < mn) mn = v;                       // gk:56-57 (strict: first occurrence kept)
+        if (v > mx) mx = v;                       // gk:58-59
+      }
+    }
+    __syncthreads();
+  }
+  if (t < nstr && L > 0) {
+    st.mn[s] = mn;
+    st.mx[s] = mx;
+    st.sum[s] = sm;
+    st.avg[s] = av;
+  }
 }
 
 // ===========================================================================
@@ -122,31 +242,34 @@ __global__ __launch_bounds__(256) void k_stats(GKState st, const double* __restr
 // The tail (values >= the last entry, rule R2) is cut into chunks of
 // max(T,1) values, each emitting (last value, chunk size, 0).
 // ===========================================================================
-// Working storage of one flush: table double buffer, per-gap scratch and the
-// pending values grouped by gap.  LDS for the 256/2048 classes, a per-block
-// global-memory workspace for the largest class (same code, address space
-// known at compile time so LDS accesses stay ds_* instructions).
+// Working storage of one flush: the table (single-buffered for the 256
+// class, whose entries a lane caches in registers; double-buffered above),
+// per-gap scratch and the pending values (members / sort area).  LDS for the
+// 256 / 2048 classes, a per-block global workspace for the largest class
+// (same code; the address space is known at compile time, so LDS accesses
+// stay ds_* instructions).
 struct FlushBuf {
-  double* tv[2];     // table values, double-buffered (old -> new)
-  int32_t* tg[2];
+  double* tv[2];     // table values: old buffer tv[cur], new buffer tv[cur^1]
+  int32_t* tg[2];    //   (both the same array when single-buffered)
   int32_t* td[2];
   uint32_t* gpk;     // per gap: count, then packed (gap base << 16) | out base
   int32_t* gk;       // per entry: absorbed count k | KEEP bit
   int32_t* gdel;     // per entry: G, then delta of emitted gap values G+d-1
-  double* mv;        // pending values grouped by gap (unsorted inside a gap)
-  int32_t* mi;       // their insertion indices (stable tie-break, gk:72)
+  double* mv;        // pending values: grouped by gap, or the sort keys
+  uint32_t* mp;      // their payload (insertion index << 16) | gap
 };
 
 template <int CAP, int VPL>
 struct FlushLDS {
-  double tv[2][CAP];
-  int32_t tg[2][CAP];
-  int32_t td[2][CAP];
+  static constexpr int NB = CAP <= 256 ? 1 : 2;
+  double tv[NB][CAP];
+  int32_t tg[NB][CAP];
+  int32_t td[NB][CAP];
   uint32_t gpk[CAP + 1];
   int32_t gk[CAP + 1];
   int32_t gdel[CAP + 1];
   double mv[64 * VPL];
-  int32_t mi[64 * VPL];
+  uint32_t mp[64 * VPL];
 };
 
 // bytes of one block's global workspace for capacity `cap`
@@ -169,59 +292,116 @@ __device__ inline FlushBuf flush_buf_global(unsigned char* base, int cap, int vp
   b.gpk = (uint32_t*)ip; ip += cap + 1;
   b.gk = ip; ip += cap + 1;
   b.gdel = ip; ip += cap + 1;
-  b.mi = ip;
+  b.mp = (uint32_t*)ip;
   return b;
 }
 
 template <int CAP, int VPL>
 __device__ inline FlushBuf flush_buf_lds(FlushLDS<CAP, VPL>& L) {
+  constexpr int NB = FlushLDS<CAP, VPL>::NB;
   FlushBuf b;
-  b.tv[0] = L.tv[0]; b.tv[1] = L.tv[1];
-  b.tg[0] = L.tg[0]; b.tg[1] = L.tg[1];
-  b.td[0] = L.td[0]; b.td[1] = L.td[1];
-  b.gpk = L.gpk; b.gk = L.gk; b.gdel = L.gdel; b.mv = L.mv; b.mi = L.mi;
+  b.tv[0] = L.tv[0]; b.tv[1] = L.tv[NB - 1];
+  b.tg[0] = L.tg[0]; b.tg[1] = L.tg[NB - 1];
+  b.td[0] = L.td[0]; b.td[1] = L.td[NB - 1];
+  b.gpk = L.gpk; b.gk = L.gk; b.gdel = L.gdel; b.mv = L.mv; b.mp = L.mp;
   return b;
 }
 
-// Returns the new table size, or -1 if it would exceed CAP (nothing is
-// written to the new buffer in that case).  `cur` selects the old buffer; on
-// success the new table is in buffer cur^1.
-template <int VPL>
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, DPP_ROW_SHR(1), 0xf, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, DPP_ROW_SHR(2), 0xf, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, DPP_ROW_SHR(4), 0xf, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, DPP_ROW_SHR(8), 0xf, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, DPP_ROW_BCAST15, 0xa, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, DPP_ROW_BCAST31, 0xc, 0xf, false));
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+// Gap sizes above this use the bitonic sort instead of the per-gap rank loop.
+#define GK_RANK_LOOP_MAX 24
+#define GK_PAD_PAYLOAD 0xFFFF0000u  // sorts after every real value (idx < 0xFFFF)
+
+// x (insertion index i, gap `gap`, rank `rk` inside its gap): gk:93-99 for
+// gap < E (the k smallest are absorbed, the rest emitted as (x, 1, G+d-1)),
+// gk:85-92 for the tail (chunks of max(T,1): emit each chunk's last value).
+__device__ __forceinline__ void emit_value(const FlushBuf& L, double* nv, int32_t* ng, int32_t* nd, int E,
+                                           int totm, int cs, double x, int gap, int rk) {
+  const uint32_t pk = L.gpk[gap];
+  if (gap < E) {
+    const int k = L.gk[gap] & ~GK_KEEP_BIT;
+    if (rk >= k) {
+      const int pos = (int)(pk & 0xffffu) + rk - k;
+      nv[pos] = x;
+      ng[pos] = 1;
+      nd[pos] = L.gdel[gap];
+    }
+  } else {
+    const int m = totm - (int)(pk >> 16);
+    const int q = rk / cs;
+    const int rr = rk - q * cs;
+    if (rr == cs - 1 || rk == m - 1) {
+      const int pos = (int)(pk & 0xffffu) + q;
+      nv[pos] = x;
+      ng[pos] = rr + 1;
+      nd[pos] = 0;
+    }
+  }
+}
+
+// Returns the new table size, or -1 if it would exceed `cap` (nothing is
+// written to the table in that case).  `cur` selects the old buffer; on
+// success the new table is in buffer cur^1 (the same buffer when KMAX > 0).
+// KMAX > 0: the lane's block of at most KMAX entries is cached in registers
+// and the table is updated in place.
+// `after_search` runs once every lane has read the old table for the gap
+// search; k_ingest issues the next flush's value loads there, so that the
+// compiler's first vmcnt wait for them lands in the NEXT flush.
+template <int VPL, bool GLOBAL, int KMAX, typename AfterSearch>
 __device__ __forceinline__ int flush_wave(const FlushBuf& L, const int cap, const int cur, const int E,
                                           const double (&xv)[VPL], const int cnt, const int T,
-                                          const int lane) {
-  const double* __restrict__ tv = L.tv[cur];
-  const int32_t* __restrict__ tg = L.tg[cur];
-  const int32_t* __restrict__ td = L.td[cur];
-  double* __restrict__ nv = L.tv[cur ^ 1];
-  int32_t* __restrict__ ng = L.tg[cur ^ 1];
-  int32_t* __restrict__ nd = L.td[cur ^ 1];
+                                          const int lane, AfterSearch&& after_search) {
+  constexpr bool REGS = KMAX > 0;
+  // selects, not L.tv[cur]: a runtime index into the pointer pair would put
+  // the pair in scratch memory
+  const double* __restrict__ tv = cur ? L.tv[1] : L.tv[0];
+  const int32_t* __restrict__ tg = cur ? L.tg[1] : L.tg[0];
+  const int32_t* __restrict__ td = cur ? L.td[1] : L.td[0];
+  double* __restrict__ nv = cur ? L.tv[0] : L.tv[1];
+  int32_t* __restrict__ ng = cur ? L.tg[0] : L.tg[1];
+  int32_t* __restrict__ nd = cur ? L.td[0] : L.td[1];
 
   // ---- gap of each pending value: number of entries <= x (gk:93 '<' puts
-  //      a value equal to an entry after that entry) -------------------------
+  //      a value equal to an entry after that entry); the VPL searches
+  //      advance in lock step so their LDS reads overlap -------------------
   int xg[VPL];
-  const int top = E ? (1 << (31 - __clz(E))) : 0;
 #pragma unroll
-  for (int r = 0; r < VPL; ++r) {
-    int pos = 0;
-    const double x = xv[r];
-    for (int step = top; step > 0; step >>= 1) {
-      const int pr = pos + step;
-      if (pr <= E && tv[pr - 1] <= x) pos = pr;
+  for (int r = 0; r < VPL; ++r) xg[r] = 0;
+  for (int step = E ? (1 << (31 - __clz(E))) : 0; step > 0; step >>= 1) {
+    double tvv[VPL];
+#pragma unroll
+    for (int r = 0; r < VPL; ++r) tvv[r] = tv[max(min(xg[r] + step, E) - 1, 0)];
+#pragma unroll
+    for (int r = 0; r < VPL; ++r) {
+      const int pr = xg[r] + step;
+      xg[r] = (pr <= E && tvv[r] <= xv[r]) ? pr : xg[r];
     }
-    xg[r] = pos;
   }
+  after_search();
   for (int j = lane; j <= E; j += 64) L.gpk[j] = 0u;
-  __syncthreads();
+  wsync<GLOBAL>();
   uint32_t xs[VPL];
 #pragma unroll
   for (int r = 0; r < VPL; ++r) {
     const int i = lane + 64 * r;
     xs[r] = (i < cnt) ? atomicAdd(&L.gpk[xg[r]], 1u) : 0u;
   }
-  __syncthreads();
+  wsync<GLOBAL>();
+  uint32_t mloc = 0;
+#pragma unroll
+  for (int r = 0; r < VPL; ++r) mloc = max(mloc, xs[r] + 1u);
+  const bool use_sort = wave_max_u32(mloc) > GK_RANK_LOOP_MAX;
 
-  // ---- carry walk over the entries -----------------------------------------
+  // ---- carry walk over the entries (closed form of gk:93-106) --------------
   // Lane l owns the contiguous block [l*K, l*K+K).  A lane can run its block
   // once its carry-in is known: lane 0, or a lane whose predecessor entry is
   // kept even with carry 0 (then it is kept for any carry, because G grows
@@ -230,6 +410,8 @@ __device__ __forceinline__ int flush_wave(const FlushBuf& L, const int cap, cons
   const int j0 = lane * K;
   const int jend = min(j0 + K, E);
   const bool has = j0 < E;
+  const int cs = T > 1 ? T : 1;
+  const int tail_lane = E == 0 ? 0 : (E - 1) / K;
   bool known = (lane == 0) || !has;
   if (has && lane > 0) {
     const int jp = j0 - 1;
@@ -239,121 +421,221 @@ __device__ __forceinline__ int flush_wave(const FlushBuf& L, const int cap, cons
   }
   bool done = !has;
   int cin = 0, cout = 0;
-  for (;;) {
-    if (known && !done) {
-      int c = cin;
-      for (int j = j0; j < jend; ++j) {
-        const int g = tg[j], d = td[j], m = (int)L.gpk[j];
-        const int Gp = g + c;
-        const int k = clampi(T - d - Gp, 0, m);
-        const int G = Gp + k;
-        const bool rem = (j + 1 < E) && (G + tg[j + 1] + td[j + 1] <= T);
-        L.gk[j] = k | (rem ? 0 : GK_KEEP_BIT);
-        L.gdel[j] = G;
-        c = rem ? G : 0;
+  uint32_t incl, total;
+  int newE;
+  if constexpr (REGS) {
+    double ev[KMAX];
+    int eg[KMAX], ed[KMAX], em[KMAX], eh[KMAX], eG[KMAX], ek[KMAX];
+    bool ekeep[KMAX];
+#pragma unroll
+    for (int e = 0; e < KMAX; ++e) {
+      const int j = j0 + e;
+      const bool v = e < K && j < E;
+      ev[e] = v ? tv[j] : 0.0;
+      eg[e] = v ? tg[j] : 0;
+      ed[e] = v ? td[j] : 0;
+      em[e] = v ? (int)L.gpk[j] : 0;
+      eh[e] = (v && j + 1 < E) ? tg[j + 1] + td[j + 1] : -1;  // -1: no successor
+      eG[e] = 0;
+      ek[e] = 0;
+      ekeep[e] = false;
+    }
+    for (;;) {
+      if (known && !done) {
+        int c = cin;
+#pragma unroll
+        for (int e = 0; e < KMAX; ++e) {
+          if (e < K && j0 + e < E) {
+            const int Gp = eg[e] + c;
+            const int k = clampi(T - ed[e] - Gp, 0, em[e]);
+            const int G = Gp + k;
+            const bool rem = eh[e] >= 0 && (G + eh[e] <= T);
+            eG[e] = G;
+            ek[e] = k;
+            ekeep[e] = !rem;
+            c = rem ? G : 0;
+          }
+        }
+        cout = c;
+        done = true;
       }
-      cout = c;
-      done = true;
+      const int pc = wave_shr1(cout, 0);
+      const int pd = wave_shr1((int)done, 1);
+      if (!known && pd) {
+        known = true;
+        cin = pc;
+      }
+      if (__all(done)) break;
     }
-    const int pc = __shfl_up(cout, 1, 64);
-    const int pd = __shfl_up((int)done, 1, 64);
-    if (!known && pd) {
-      known = true;
-      cin = pc;
+    uint32_t sm = 0, so = 0;
+#pragma unroll
+    for (int e = 0; e < KMAX; ++e)
+      if (e < K && j0 + e < E) {
+        sm += (uint32_t)em[e];
+        so += (uint32_t)(em[e] - ek[e] + (ekeep[e] ? 1 : 0));
+      }
+    if (lane == tail_lane) {
+      const int mE = (int)L.gpk[E];
+      sm += (uint32_t)mE;
+      so += (uint32_t)((mE + cs - 1) / cs);
     }
-    if (__all(done)) break;
-  }
-
-  // ---- output counts: gap j emits m_j - k_j values, then entry j if kept;
-  //      the tail emits ceil(m_E / max(T,1)) chunk ends -----------------------
-  const int cs = T > 1 ? T : 1;
-  const int tail_lane = E == 0 ? 0 : (E - 1) / K;
-  uint32_t sm = 0, so = 0;
-  for (int j = j0; j < jend; ++j) {
-    const int m = (int)L.gpk[j];
-    const int kk = L.gk[j];
-    sm += (uint32_t)m;
-    so += (uint32_t)(m - (kk & ~GK_KEEP_BIT) + ((kk & GK_KEEP_BIT) ? 1 : 0));
-  }
-  int mE = 0;
-  if (lane == tail_lane) {
-    mE = (int)L.gpk[E];
-    sm += (uint32_t)mE;
-    so += (uint32_t)((mE + cs - 1) / cs);
-  }
-  const uint32_t incl = wave_incl_scan_u32((sm << 16) | so, lane);
-  const uint32_t total = __shfl(incl, 63, 64);
-  const int newE = (int)(total & 0xffffu);
-  if (newE > cap) return -1;
-  uint32_t base = incl - ((sm << 16) | so);
-  for (int j = j0; j < jend; ++j) {
-    const int m = (int)L.gpk[j];
-    const int kk = L.gk[j];
-    const int k = kk & ~GK_KEEP_BIT;
-    const int G = L.gdel[j];
-    const int d = td[j];
-    L.gpk[j] = base;
-    L.gdel[j] = G + d - 1;
-    const int ob = (int)(base & 0xffffu);
-    if (kk & GK_KEEP_BIT) {
-      const int pos = ob + m - k;
-      nv[pos] = tv[j];
-      ng[pos] = G;
-      nd[pos] = d;
+    incl = wave_incl_scan_u32((sm << 16) | so, lane);
+    total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    newE = (int)(total & 0xffffu);
+    if (newE > cap) return -1;
+    wsync<GLOBAL>();  // every lane has read the old table and the counts
+    uint32_t base = incl - ((sm << 16) | so);
+#pragma unroll
+    for (int e = 0; e < KMAX; ++e)
+      if (e < K && j0 + e < E) {
+        const int j = j0 + e;
+        L.gpk[j] = base;
+        L.gk[j] = ek[e] | (ekeep[e] ? GK_KEEP_BIT : 0);
+        L.gdel[j] = eG[e] + ed[e] - 1;
+        if (ekeep[e]) {
+          const int pos = (int)(base & 0xffffu) + em[e] - ek[e];
+          nv[pos] = ev[e];
+          ng[pos] = eG[e];
+          nd[pos] = ed[e];
+        }
+        base += ((uint32_t)em[e] << 16) | (uint32_t)(em[e] - ek[e] + (ekeep[e] ? 1 : 0));
+      }
+    if (lane == tail_lane) L.gpk[E] = base;
+  } else {
+    for (;;) {
+      if (known && !done) {
+        int c = cin;
+        for (int j = j0; j < jend; ++j) {
+          const int g = tg[j], d = td[j], m = (int)L.gpk[j];
+          const int Gp = g + c;
+          const int k = clampi(T - d - Gp, 0, m);
+          const int G = Gp + k;
+          const bool rem = (j + 1 < E) && (G + tg[j + 1] + td[j + 1] <= T);
+          L.gk[j] = k | (rem ? 0 : GK_KEEP_BIT);
+          L.gdel[j] = G;
+          c = rem ? G : 0;
+        }
+        cout = c;
+        done = true;
+      }
+      const int pc = wave_shr1(cout, 0);
+      const int pd = wave_shr1((int)done, 1);
+      if (!known && pd) {
+        known = true;
+        cin = pc;
+      }
+      if (__all(done)) break;
     }
-    base += ((uint32_t)m << 16) | (uint32_t)(m - k + ((kk & GK_KEEP_BIT) ? 1 : 0));
+    uint32_t sm = 0, so = 0;
+    for (int j = j0; j < jend; ++j) {
+      const int m = (int)L.gpk[j];
+      const int kk = L.gk[j];
+      sm += (uint32_t)m;
+      so += (uint32_t)(m - (kk & ~GK_KEEP_BIT) + ((kk & GK_KEEP_BIT) ? 1 : 0));
+    }
+    if (lane == tail_lane) {
+      const int mE = (int)L.gpk[E];
+      sm += (uint32_t)mE;
+      so += (uint32_t)((mE + cs - 1) / cs);
+    }
+    incl = wave_incl_scan_u32((sm << 16) | so, lane);
+    total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    newE = (int)(total & 0xffffu);
+    if (newE > cap) return -1;
+    uint32_t base = incl - ((sm << 16) | so);
+    for (int j = j0; j < jend; ++j) {
+      const int m = (int)L.gpk[j];
+      const int kk = L.gk[j];
+      const int k = kk & ~GK_KEEP_BIT;
+      const int G = L.gdel[j];
+      const int d = td[j];
+      L.gpk[j] = base;
+      L.gdel[j] = G + d - 1;
+      if (kk & GK_KEEP_BIT) {
+        const int pos = (int)(base & 0xffffu) + m - k;
+        nv[pos] = tv[j];
+        ng[pos] = G;
+        nd[pos] = d;
+      }
+      base += ((uint32_t)m << 16) | (uint32_t)(m - k + ((kk & GK_KEEP_BIT) ? 1 : 0));
+    }
+    if (lane == tail_lane) L.gpk[E] = base;
   }
-  if (lane == tail_lane) L.gpk[E] = base;
   const int totm = (int)(total >> 16);
-  __syncthreads();
+  wsync<GLOBAL>();
 
-  // ---- stable order inside each gap, then emit the surviving values --------
+  // ---- stable order inside each gap (gk:72), then emit --------------------
+  if (!use_sort) {
+    // small gaps: scatter by gap, rank by comparison with the gap's members
 #pragma unroll
-  for (int r = 0; r < VPL; ++r) {
-    const int i = lane + 64 * r;
-    if (i < cnt) {
-      const int pos = (int)(L.gpk[xg[r]] >> 16) + (int)xs[r];
-      L.mv[pos] = xv[r];
-      L.mi[pos] = i;
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < VPL; ++r) {
-    const int i = lane + 64 * r;
-    if (i < cnt) {
-      const int gap = xg[r];
-      const uint32_t pk = L.gpk[gap];
-      const int gb = (int)(pk >> 16);
-      const int ge = gap < E ? (int)(L.gpk[gap + 1] >> 16) : totm;
-      const double x = xv[r];
-      int rk = 0;
-      for (int t = gb; t < ge; ++t) {
-        const double y = L.mv[t];
-        rk += (y < x) || (y == x && L.mi[t] < i);
-      }
-      if (gap < E) {
-        const int k = L.gk[gap] & ~GK_KEEP_BIT;
-        if (rk >= k) {
-          const int pos = (int)(pk & 0xffffu) + rk - k;
-          nv[pos] = x;
-          ng[pos] = 1;
-          nd[pos] = L.gdel[gap];
-        }
-      } else {
-        const int m = ge - gb;
-        const int q = rk / cs;
-        const int rr = rk - q * cs;
-        if (rr == cs - 1 || rk == m - 1) {
-          const int pos = (int)(pk & 0xffffu) + q;
-          nv[pos] = x;
-          ng[pos] = rr + 1;
-          nd[pos] = 0;
-        }
+    for (int r = 0; r < VPL; ++r) {
+      const int i = lane + 64 * r;
+      if (i < cnt) {
+        const int pos = (int)(L.gpk[xg[r]] >> 16) + (int)xs[r];
+        L.mv[pos] = xv[r];
+        L.mp[pos] = (uint32_t)i;
       }
     }
+    wsync<GLOBAL>();
+#pragma unroll
+    for (int r = 0; r < VPL; ++r) {
+      const int i = lane + 64 * r;
+      if (i < cnt) {
+        const int gap = xg[r];
+        const int gb = (int)(L.gpk[gap] >> 16);
+        const int ge = gap < E ? (int)(L.gpk[gap + 1] >> 16) : totm;
+        const double x = xv[r];
+        int rk = 0;
+        for (int t = gb; t < ge; ++t) {
+          const double y = L.mv[t];
+          rk += (y < x) || (y == x && (int)L.mp[t] < i);
+        }
+        emit_value(L, nv, ng, nd, E, totm, cs, x, gap, rk);
+      }
+    }
+  } else {
+    // a large gap (first flush: everything is tail; adversarial orders):
+    // bitonic sort of all values by (value, insertion index); all values of
+    // gap g precede those of gap g+1, so rank = sorted position - gap base
+    constexpr int N = 64 * VPL;
+#pragma unroll
+    for (int r = 0; r < VPL; ++r) {
+      const int i = lane + 64 * r;
+      L.mv[i] = (i < cnt) ? xv[r] : __longlong_as_double(0x7ff0000000000000LL);
+      L.mp[i] = (i < cnt) ? (((uint32_t)i << 16) | (uint32_t)xg[r]) : GK_PAD_PAYLOAD;
+    }
+    wsync<GLOBAL>();
+    for (int k = 2; k <= N; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int pp = lane; pp < N / 2; pp += 64) {
+          const int i = ((pp & ~(j - 1)) << 1) | (pp & (j - 1));
+          const int l = i + j;
+          const double a = L.mv[i], b = L.mv[l];
+          const uint32_t pa = L.mp[i], pb = L.mp[l];
+          const bool a_gt = (a > b) || (a == b && (pa >> 16) > (pb >> 16));
+          const bool asc = (i & k) == 0;
+          if (a_gt == asc) {
+            L.mv[i] = b;
+            L.mv[l] = a;
+            L.mp[i] = pb;
+            L.mp[l] = pa;
+          }
+        }
+        wsync<GLOBAL>();
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < VPL; ++r) {
+      const int q = lane + 64 * r;
+      if (q < cnt) {
+        const double x = L.mv[q];
+        const int gap = (int)(L.mp[q] & 0xffffu);
+        const int rk = q - (int)(L.gpk[gap] >> 16);
+        emit_value(L, nv, ng, nd, E, totm, cs, x, gap, rk);
+      }
+    }
   }
-  __syncthreads();
+  wsync<GLOBAL>();
   return newE;
 }
 
@@ -369,6 +651,7 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
                                                int32_t* __restrict__ ovf_list) {
   constexpr int LCAP = CAP > 0 ? CAP : 1;
   constexpr int LVPL = CAP > 0 ? VPL : 1;
+  constexpr int KMAX = CAP == 256 ? 4 : 0;  // registers cache a lane's block of entries
   __shared__ FlushLDS<LCAP, LVPL> Ls;
   FlushBuf B;
   if constexpr (CAP > 0) {
@@ -381,64 +664,90 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
   const int P = st.P;
   for (int64_t w = blockIdx.x; w < count; w += gridDim.x) {
     const int64_t s = list ? (int64_t)list[w] : w;
-    if (!list && st.cls[s] != 0) continue;  // promoted: handled by its class launch
-    int64_t xo = 0, Lx = 0;
-    if (x) {
-      xo = offs[s];
-      Lx = offs[s + 1] - xo;
-    }
+    // header: every load issued before the first use (one round trip);
+    // flush-only launches pass x == NULL and an all-zero offs array
+    const int32_t scls = st.cls[s];
+    const int64_t xo = offs[s];
+    const int64_t xe = offs[s + 1];
     int p = st.pend[s];
     int64_t n = st.n[s];
+    int E = st.E[s];
+    if (!list && scls != 0) continue;  // promoted: handled by its class launch
+    const int64_t Lx = xe - xo;
     // force 1: flush only if values are pending (size/quantile, gk:45, 166, 197)
     // force 2: unconditional merge_compress() (merge, gk:122, 126, 137)
     if (Lx <= 0 && !((force == 1 && p > 0) || (force == 2 && n > 0))) continue;
     GKRec* __restrict__ tab = gk_table_ptr(st, s);
     double* __restrict__ pb = st.pbuf + s * (int64_t)st.pmax;
-    int E = st.E[s];
     int cur = 0;
-    for (int j = lane; j < E; j += 64) {
-      const GKRec rc = tab[j];
-      B.tv[0][j] = rc.v;
-      B.tg[0][j] = rc.g;
-      B.td[0][j] = rc.d;
+    // table -> LDS: all of a lane's loads are issued before the first wait
+    constexpr int TL = CAP > 0 ? CAP / 64 : 8;
+    for (int j0 = 0; j0 < E; j0 += 64 * TL) {
+      GKRec rc[TL];
+#pragma unroll
+      for (int r = 0; r < TL; ++r) {
+        const int j = j0 + lane + 64 * r;
+        if (j < E) rc[r] = tab[j];
+      }
+#pragma unroll
+      for (int r = 0; r < TL; ++r) {
+        const int j = j0 + lane + 64 * r;
+        if (j < E) {
+          B.tv[0][j] = rc[r].v;
+          B.tg[0][j] = rc[r].g;
+          B.td[0][j] = rc[r].d;
+        }
+      }
     }
-    __syncthreads();
+    wsync<CAP == 0>();
 
     bool ok = true;
+    bool flushed = false;  // at least one automatic flush in this call
     int64_t used = 0;
     int64_t need = P - (n % P);  // adds until n hits the next multiple of P (gk:60)
+    // The values of the next flush (or the leftover tail of the batch) are
+    // loaded one flush ahead: their HBM latency hides under the current
+    // flush's LDS work.
+    double xv[VPL];
+    if (used + need <= Lx) gk_load_flush_values<VPL>(xv, pb, p, x + xo, p + (int)need, lane);
     while (used + need <= Lx) {
       const int cnt = p + (int)need;
-      double xv[VPL];
+      const int64_t nused = used + need;
+      const int navail = (int)min((int64_t)P, Lx - nused);  // next flush, or the leftover tail
+      double xn[VPL];
+      auto prefetch = [&]() {
+        if (navail > 0) {
+          const double* base = x + xo + nused;
 #pragma unroll
-      for (int r = 0; r < VPL; ++r) {
-        const int i = lane + 64 * r;
-        xv[r] = (i < p) ? pb[i] : ((i < cnt) ? x[xo + used + (i - p)] : 0.0);
-      }
+          for (int r = 0; r < VPL; ++r) gk_load_async(xn[r], base + min(lane + 64 * r, navail - 1));
+        }
+      };
       n += need;
-      const int nE = flush_wave<VPL>(B, cap, cur, E, xv, cnt, gk_threshold(st, n), lane);
+      const int nE = flush_wave<VPL, CAP == 0, KMAX>(B, cap, cur, E, xv, cnt, gk_threshold(st, n), lane, prefetch);
+      // retire the prefetch on EVERY path: a load still in flight when its
+      // registers are reused would overwrite whatever the compiler put there
+      if (navail > 0) gk_vm_wait<VPL>(xn);
       if (nE < 0) {
         ok = false;
         break;
       }
       E = nE;
       cur ^= 1;
-      used += need;
+      used = nused;
       p = 0;
       need = P;
+      flushed = true;
+#pragma unroll
+      for (int r = 0; r < VPL; ++r) xv[r] = (lane + 64 * r < navail) ? xn[r] : 0.0;
     }
     if (ok) {
       const int64_t rem = Lx - used;  // < need: no automatic flush for these
+      // after an automatic flush the leftover values are already in xv
       if ((force == 1 && p + rem > 0) || force == 2) {
         const int cnt = p + (int)rem;
-        double xv[VPL];
-#pragma unroll
-        for (int r = 0; r < VPL; ++r) {
-          const int i = lane + 64 * r;
-          xv[r] = (i < p) ? pb[i] : ((i < cnt) ? x[xo + used + (i - p)] : 0.0);
-        }
+        if (!flushed) gk_load_flush_values<VPL>(xv, pb, p, x ? x + xo + used : pb, cnt, lane);
         n += rem;
-        const int nE = flush_wave<VPL>(B, cap, cur, E, xv, cnt, gk_threshold(st, n), lane);
+        const int nE = flush_wave<VPL, CAP == 0, KMAX>(B, cap, cur, E, xv, cnt, gk_threshold(st, n), lane, [] {});
         if (nE < 0) {
           ok = false;
         } else {
@@ -447,7 +756,13 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
           p = 0;
         }
       } else {
-        for (int64_t i = lane; i < rem; i += 64) pb[p + i] = x[xo + used + i];
+        if (flushed) {
+#pragma unroll
+          for (int r = 0; r < VPL; ++r)
+            if (lane + 64 * r < rem) pb[lane + 64 * r] = xv[r];
+        } else {
+          for (int64_t i = lane; i < rem; i += 64) pb[p + i] = x[xo + used + i];
+        }
         p += (int)rem;
         n += rem;
       }
@@ -459,22 +774,27 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
         const int k = atomicAdd(ovf_count, 1);
         ovf_list[k] = (int32_t)s;
       }
-      __syncthreads();
+      wsync<CAP == 0>();
       continue;
     }
-    for (int j = lane; j < E; j += 64) {
-      GKRec rc;
-      rc.v = B.tv[cur][j];
-      rc.g = B.tg[cur][j];
-      rc.d = B.td[cur][j];
-      tab[j] = rc;
+    {
+      const double* fv = cur ? B.tv[1] : B.tv[0];
+      const int32_t* fg = cur ? B.tg[1] : B.tg[0];
+      const int32_t* fd = cur ? B.td[1] : B.td[0];
+      for (int j = lane; j < E; j += 64) {
+        GKRec rc;
+        rc.v = fv[j];
+        rc.g = fg[j];
+        rc.d = fd[j];
+        tab[j] = rc;
+      }
     }
     if (lane == 0) {
       st.n[s] = n;
       st.E[s] = E;
       st.pend[s] = p;
     }
-    __syncthreads();
+    wsync<CAP == 0>();
   }
 }
 

@@ -350,6 +350,7 @@ def test_large_batch_properties_and_sample(gpu_device):
     o.ingest(xs.reshape(-1), np.arange(0, len(idx) * L + 1, L))
     oq = o.quantiles([0.5, 0.9, 0.99])
     assert_same_quantiles(q.cpu().numpy()[idx], oq, "sample quantiles")
+    offs_t, v, gg, dd = ss.tables()  # after the query flush, like the oracle's
     go, gv, ggn, gdn = offs_t.cpu().numpy(), v.cpu().numpy(), gg.cpu().numpy(), dd.cpu().numpy()
     oo, ov, og, od = o.tables()
     for k, s in enumerate(idx[:500]):
