@@ -108,42 +108,58 @@ __device__ __forceinline__ void wsync() {
 
 
 // ---------------------------------------------------------------------------
-// Explicit prefetch.  hipcc's waitcnt pass is conservative across loop
-// iterations: a register loaded in iteration k and used in k+1 gets a
-// vmcnt(0) wait in front of its first use, which also waits for every load
-// issued since.  These loads are invisible to that pass; the consumer waits
-// with gk_vm_wait(), which ties the registers so no use moves above it.
-// (Correctness of the compiler's own counted waits is unaffected: loads retire
-// in order, so extra outstanding loads only make its vmcnt(N) stricter.)
+// Loads of flush values.  All loads are ordinary (compiler-visible): the
+// compiler then places the vmcnt wait at the first use.  The prefetch of the
+// next flush is issued after the gap search of the current one, so its first
+// use -- the select at the end of the flush -- lands after the flush's LDS
+// work.  (Inline-asm loads were tried and rejected: the compiler may copy an
+// asm output register before the load lands; tools/check_async_loads.py.)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void gk_load_async(double& dst, const double* p) {
-  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(dst) : "v"(p) : "memory");
-}
-
-template <int VPL>
-__device__ __forceinline__ void gk_vm_wait(double (&v)[VPL]) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int r = 0; r < VPL; ++r) asm volatile("" : "+v"(v[r]));
-}
-
-
 // A flush's values: the first p come from the stream's pending buffer, the
-// rest from the batch.  Loaded explicitly and waited for here, so that no
-// compiler-visible load is outstanding on these registers afterwards.
+// rest from the batch.
 template <int VPL>
 __device__ __forceinline__ void gk_load_flush_values(double (&xv)[VPL], const double* pb, int p,
                                                      const double* xs, int cnt, int lane) {
+  if (cnt <= 0) {
+#pragma unroll
+    for (int r = 0; r < VPL; ++r) xv[r] = 0.0;
+    return;
+  }
 #pragma unroll
   for (int r = 0; r < VPL; ++r) {
-    const int i = lane + 64 * r;
-    const int ic = min(i, max(cnt - 1, 0));
+    const int ic = min(lane + 64 * r, cnt - 1);
     const double* a = (ic < p) ? pb + ic : xs + (ic - p);
-    if (cnt > 0) gk_load_async(xv[r], a);
+    xv[r] = *a;
   }
-  if (cnt > 0) gk_vm_wait<VPL>(xv);
 #pragma unroll
   for (int r = 0; r < VPL; ++r) xv[r] = (lane + 64 * r < cnt) ? xv[r] : 0.0;
+}
+
+// Per-stream header, loaded for the NEXT stream while the current one is
+// processed (uniform addresses: one request each).
+struct GKHdrV {
+  int32_t cls, slot, pend, E;
+  int64_t n, xo, xe;
+};
+
+__device__ __forceinline__ void gk_hdr_issue(GKHdrV& h, const GKState& st, const int64_t* offs, int64_t s) {
+  h.cls = st.cls[s];
+  h.slot = st.slot[s];
+  h.pend = st.pend[s];
+  h.E = st.E[s];
+  h.n = st.n[s];
+  h.xo = offs[s];
+  h.xe = offs[s + 1];
+}
+
+__device__ __forceinline__ int64_t rfl64(int64_t v) {
+  const int lo = __builtin_amdgcn_readfirstlane((int)(uint32_t)(uint64_t)v);
+  const int hi = __builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+__device__ __forceinline__ GKRec* gk_table_ptr_cs(const GKState& st, int64_t s, int32_t c, int32_t slot) {
+  return c == 0 ? st.tab[0] + s * (int64_t)st.cap[0] : st.tab[c] + (int64_t)slot * st.cap[c];
 }
 
 // ===========================================================================
@@ -317,6 +333,15 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
+// smallest power of two strictly above e (e >= 0)
+__device__ __forceinline__ int gk_pow2_above(int e) { return 1 << (32 - __clz(e)); }
+
+// +inf into tv[E .. pow2_above(E)-2]: the probes of the branch-free search
+__device__ __forceinline__ void gk_pad_table(double* tv, int E, int lane) {
+  const int hi = gk_pow2_above(E) - 1;
+  for (int j = E + lane; j < hi; j += 64) tv[j] = __longlong_as_double(0x7ff0000000000000LL);
+}
+
 // Gap sizes above this use the bitonic sort instead of the per-gap rank loop.
 #define GK_RANK_LOOP_MAX 24
 #define GK_PAD_PAYLOAD 0xFFFF0000u  // sorts after every real value (idx < 0xFFFF)
@@ -373,19 +398,21 @@ __device__ __forceinline__ int flush_wave(const FlushBuf& L, const int cap, cons
   // ---- gap of each pending value: number of entries <= x (gk:93 '<' puts
   //      a value equal to an entry after that entry); the VPL searches
   //      advance in lock step so their LDS reads overlap -------------------
+  // The table is padded with +inf up to index pow2ceil(E+1)-2, so every probe
+  // is in range and the search is branch-free; a value of +inf can step into
+  // the padding, hence the final min with E.
   int xg[VPL];
 #pragma unroll
   for (int r = 0; r < VPL; ++r) xg[r] = 0;
-  for (int step = E ? (1 << (31 - __clz(E))) : 0; step > 0; step >>= 1) {
+  for (int step = gk_pow2_above(E) >> 1; step > 0; step >>= 1) {
     double tvv[VPL];
 #pragma unroll
-    for (int r = 0; r < VPL; ++r) tvv[r] = tv[max(min(xg[r] + step, E) - 1, 0)];
+    for (int r = 0; r < VPL; ++r) tvv[r] = tv[xg[r] + step - 1];
 #pragma unroll
-    for (int r = 0; r < VPL; ++r) {
-      const int pr = xg[r] + step;
-      xg[r] = (pr <= E && tvv[r] <= xv[r]) ? pr : xg[r];
-    }
+    for (int r = 0; r < VPL; ++r) xg[r] += (tvv[r] <= xv[r]) ? step : 0;
   }
+#pragma unroll
+  for (int r = 0; r < VPL; ++r) xg[r] = min(xg[r], E);
   after_search();
   for (int j = lane; j <= E; j += 64) L.gpk[j] = 0u;
   wsync<GLOBAL>();
@@ -482,7 +509,7 @@ __device__ __forceinline__ int flush_wave(const FlushBuf& L, const int cap, cons
     incl = wave_incl_scan_u32((sm << 16) | so, lane);
     total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     newE = (int)(total & 0xffffu);
-    if (newE > cap) return -1;
+    if (newE > cap - 1) return -1;  // one slot stays free for the search padding
     wsync<GLOBAL>();  // every lane has read the old table and the counts
     uint32_t base = incl - ((sm << 16) | so);
 #pragma unroll
@@ -541,7 +568,7 @@ __device__ __forceinline__ int flush_wave(const FlushBuf& L, const int cap, cons
     incl = wave_incl_scan_u32((sm << 16) | so, lane);
     total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     newE = (int)(total & 0xffffu);
-    if (newE > cap) return -1;
+    if (newE > cap - 1) return -1;  // one slot stays free for the search padding
     uint32_t base = incl - ((sm << 16) | so);
     for (int j = j0; j < jend; ++j) {
       const int m = (int)L.gpk[j];
@@ -586,9 +613,16 @@ __device__ __forceinline__ int flush_wave(const FlushBuf& L, const int cap, cons
         const int ge = gap < E ? (int)(L.gpk[gap + 1] >> 16) : totm;
         const double x = xv[r];
         int rk = 0;
-        for (int t = gb; t < ge; ++t) {
-          const double y = L.mv[t];
-          rk += (y < x) || (y == x && (int)L.mp[t] < i);
+        int t = gb;
+        for (; t + 1 < ge; t += 2) {
+          const double y0 = L.mv[t], y1 = L.mv[t + 1];
+          const int i0 = (int)L.mp[t], i1 = (int)L.mp[t + 1];
+          rk += (int)((y0 < x) | ((y0 == x) & (i0 < i)));
+          rk += (int)((y1 < x) | ((y1 == x) & (i1 < i)));
+        }
+        if (t < ge) {
+          const double y0 = L.mv[t];
+          rk += (int)((y0 < x) | ((y0 == x) & ((int)L.mp[t] < i)));
         }
         emit_value(L, nv, ng, nd, E, totm, cs, x, gap, rk);
       }
@@ -635,6 +669,7 @@ __device__ __forceinline__ int flush_wave(const FlushBuf& L, const int cap, cons
       }
     }
   }
+  gk_pad_table(nv, newE, lane);
   wsync<GLOBAL>();
   return newE;
 }
@@ -662,22 +697,28 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
   }
   const int lane = threadIdx.x;
   const int P = st.P;
-  for (int64_t w = blockIdx.x; w < count; w += gridDim.x) {
+  // headers are prefetched one stream ahead; flush-only launches pass
+  // x == NULL and an all-zero offs array
+  const int64_t G = gridDim.x;
+  GKHdrV hv;
+  if ((int64_t)blockIdx.x < count) gk_hdr_issue(hv, st, offs, list ? (int64_t)list[blockIdx.x] : (int64_t)blockIdx.x);
+  for (int64_t w = blockIdx.x; w < count; w += G) {
     const int64_t s = list ? (int64_t)list[w] : w;
-    // header: every load issued before the first use (one round trip);
-    // flush-only launches pass x == NULL and an all-zero offs array
-    const int32_t scls = st.cls[s];
-    const int64_t xo = offs[s];
-    const int64_t xe = offs[s + 1];
-    int p = st.pend[s];
-    int64_t n = st.n[s];
-    int E = st.E[s];
+    const int32_t scls = __builtin_amdgcn_readfirstlane(hv.cls);
+    const int32_t sslot = __builtin_amdgcn_readfirstlane(hv.slot);
+    int p = __builtin_amdgcn_readfirstlane(hv.pend);
+    int E = __builtin_amdgcn_readfirstlane(hv.E);
+    int64_t n = rfl64(hv.n);
+    const int64_t xo = rfl64(hv.xo);
+    const int64_t xe = rfl64(hv.xe);
+    if (w + G < count) gk_hdr_issue(hv, st, offs, list ? (int64_t)list[w + G] : w + G);
     if (!list && scls != 0) continue;  // promoted: handled by its class launch
     const int64_t Lx = xe - xo;
+
     // force 1: flush only if values are pending (size/quantile, gk:45, 166, 197)
     // force 2: unconditional merge_compress() (merge, gk:122, 126, 137)
     if (Lx <= 0 && !((force == 1 && p > 0) || (force == 2 && n > 0))) continue;
-    GKRec* __restrict__ tab = gk_table_ptr(st, s);
+    GKRec* __restrict__ tab = gk_table_ptr_cs(st, s, scls, sslot);
     double* __restrict__ pb = st.pbuf + s * (int64_t)st.pmax;
     int cur = 0;
     // table -> LDS: all of a lane's loads are issued before the first wait
@@ -699,9 +740,12 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
         }
       }
     }
+    if (E <= cap - 1) gk_pad_table(B.tv[0], E, lane);
     wsync<CAP == 0>();
 
-    bool ok = true;
+    // an imported / merged table with no room for the search padding goes
+    // straight to the overflow path (promotion)
+    bool ok = E <= cap - 1;
     bool flushed = false;  // at least one automatic flush in this call
     int64_t used = 0;
     int64_t need = P - (n % P);  // adds until n hits the next multiple of P (gk:60)
@@ -709,24 +753,23 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
     // loaded one flush ahead: their HBM latency hides under the current
     // flush's LDS work.
     double xv[VPL];
-    if (used + need <= Lx) gk_load_flush_values<VPL>(xv, pb, p, x + xo, p + (int)need, lane);
-    while (used + need <= Lx) {
+    if (ok && used + need <= Lx) gk_load_flush_values<VPL>(xv, pb, p, x + xo, p + (int)need, lane);
+    while (ok && used + need <= Lx) {
       const int cnt = p + (int)need;
       const int64_t nused = used + need;
       const int navail = (int)min((int64_t)P, Lx - nused);  // next flush, or the leftover tail
       double xn[VPL];
+#pragma unroll
+      for (int r = 0; r < VPL; ++r) xn[r] = 0.0;
       auto prefetch = [&]() {
         if (navail > 0) {
           const double* base = x + xo + nused;
 #pragma unroll
-          for (int r = 0; r < VPL; ++r) gk_load_async(xn[r], base + min(lane + 64 * r, navail - 1));
+          for (int r = 0; r < VPL; ++r) xn[r] = base[min(lane + 64 * r, navail - 1)];
         }
       };
       n += need;
       const int nE = flush_wave<VPL, CAP == 0, KMAX>(B, cap, cur, E, xv, cnt, gk_threshold(st, n), lane, prefetch);
-      // retire the prefetch on EVERY path: a load still in flight when its
-      // registers are reused would overwrite whatever the compiler put there
-      if (navail > 0) gk_vm_wait<VPL>(xn);
       if (nE < 0) {
         ok = false;
         break;
@@ -973,7 +1016,7 @@ __global__ __launch_bounds__(64) void k_merge(MergeArgs a) {
   for (int64_t w = blockIdx.x; w < a.count; w += gridDim.x) {
     const int64_t s = a.list ? (int64_t)a.list[w] : w;
     GKRec* __restrict__ tab = gk_table_ptr(st, s);
-    const int outcap = min(st.cap[st.cls[s]], CAPL);
+    const int outcap = min(st.cap[st.cls[s]], CAPL) - 1;  // k_ingest keeps one slot for padding
     int64_t n = st.n[s];
     const int E = st.E[s];
     const int p = st.pend[s];
@@ -1231,7 +1274,7 @@ __global__ void k_import(GKState st, const int64_t* __restrict__ offs, const dou
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t s = wave; s < st.S; s += nw) {
-    const int cap = st.cap[st.cls[s]];
+    const int cap = st.cap[st.cls[s]] - 1;  // k_ingest keeps one slot for padding
     const int64_t o = offs[s];
     const int E = (int)(offs[s + 1] - o);
     const int64_t po = poffs[s];

@@ -74,7 +74,8 @@ def load(path=None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    # GK_LIB_PATH selects an alternative build (A/B experiments); default in-tree
+    p = path or os.environ.get("GK_LIB_PATH") or LIB_PATH
     if not os.path.exists(p):
         raise GKBackendError(GK_E_HIP, "HIP library not built: %s (run __graft_entry__.build())" % p)
     try:

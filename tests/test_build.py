@@ -1,0 +1,51 @@
+"""Build-level invariants of the HIP kernels (no GPU needed: hipcc
+cross-compiles for gfx950 here)."""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "sketches-py_amd", "csrc")
+
+
+@pytest.fixture(scope="module")
+def resource_report(tmp_path_factory):
+    out = tmp_path_factory.mktemp("res") / "k.o"
+    r = subprocess.run(
+        ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
+         "-Wno-unused-result", "-I" + os.path.join(ROOT, "include"), "-I" + CSRC,
+         "-Rpass-analysis=kernel-resource-usage", "-c", os.path.join(CSRC, "gk_kernels.hip"), "-o", str(out)],
+        capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    kernels = {}
+    cur = None
+    for line in r.stderr.splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            cur = m.group(1)
+            kernels[cur] = {}
+            continue
+        m = re.search(r"remark:\s+(.+?): (\d+) \[", line)
+        if cur and m:
+            kernels[cur][m.group(1).strip()] = int(m.group(2))
+    return kernels
+
+
+def test_ingest_kernels_do_not_spill(resource_report):
+    """k_ingest issues asm loads whose registers are waited for explicitly
+    (gk_load_async / gk_vm_wait); a VGPR spill would read such a register
+    before its load lands.  Every k_ingest instantiation must have zero
+    scratch."""
+    ingest = {k: v for k, v in resource_report.items() if "k_ingest" in k}
+    assert len(ingest) >= 10
+    bad = {k: v.get("ScratchSize [bytes/lane]") for k, v in ingest.items()
+           if v.get("ScratchSize [bytes/lane]", 0) != 0 or v.get("VGPRs Spill", 0) != 0}
+    assert not bad, bad
+
+
+def test_fast_class_occupancy(resource_report):
+    k = [v for n, v in resource_report.items() if n.startswith("_Z8k_ingestILi256ELi2E")][0]
+    assert k["Occupancy [waves/SIMD]"] >= 3
+    assert k["LDS Size [bytes/block]"] <= 9 * 1024
