@@ -5,10 +5,11 @@ the fraction of the HBM roofline reached by the dominant kernel (k_ingest).
 
 Workload (BASELINE.json configs[2], the metric's configuration, which fits one
 GPU): 1,000,000 streams x 1,000 Pareto(1.5)+1 float64 values per GPU, eps=0.01.
-One step = reset every sketch, ingest the whole batch (k_stats + k_ingest: 9
-automatic flushes per stream at the reference's flush points) and answer
-quantiles([0.5, 0.9, 0.99]) for every stream (which flushes the 91 pending
-values first, gk:197).  Inputs are generated on the GPU (synthetic, seeded)
+One step = reset every sketch, ingest the whole batch and answer
+quantiles([0.5, 0.9, 0.99]) for every stream: k_stats (n/sum/avg/min/max
+chain) then one k_ingest pass (9 automatic flushes per stream at the
+reference's flush points, then the query flush of the 91 pending values,
+gk:197, and the rank walk from the on-chip table).  Inputs are generated on the GPU (synthetic, seeded)
 and are resident in HBM before the timed region.  Multi-GPU: every rank runs
 its own 1M-stream shard (streams are independent: weak scaling, no collective
 on the data path); value = all ranks' values / max-over-ranks time.
@@ -29,7 +30,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, MI355X_MICROARCH.md "Chip-level parameters"
-HEADER_BYTES = 36       # per stream touched by k_ingest: slot1, n, E, pend read + n, E, pend written
+HEADER_BYTES = 60       # per stream: cls, slot, pend, E, n, offs pair, min, max read; n, E, pend written
 
 
 def parse():
@@ -58,15 +59,17 @@ def make_input(S, L, seed, device):
     return x, offs
 
 
-def algorithmic_bytes(ss, S, N):
-    """Bytes one k_ingest launch must move on a fresh batch:
-    8 B per value + offsets + per stream 16 B per table entry read and written
-    + 8 B per pending value read and written + the header words."""
+def algorithmic_bytes(ss, S, N, nq):
+    """Bytes one fused k_ingest launch must move on a fresh batch (SURVEY
+    8(d)): 8 B per value + offsets + 16 B per table entry read and written +
+    8 B per pending value read and written + the header words + 8 B per
+    quantile answer.  Sizes are read after an untimed identical step."""
     st = ss.stats()
     e_out = int(st["size"].to(torch.int64).sum().item())
-    p_out = int(st["pending"].to(torch.int64).sum().item())
+    p_out = int(st["pending"].to(torch.int64).sum().item())  # 0: the query flushed them
     e_in = p_in = 0  # every step starts from reset sketches
-    return 8 * N + 8 * (S + 1) + 16 * (e_in + e_out) + 8 * (p_in + p_out) + HEADER_BYTES * S
+    return (8 * N + 8 * (S + 1) + 16 * (e_in + e_out) + 8 * (p_in + p_out) + HEADER_BYTES * S
+            + 8 * nq * S)
 
 
 def cpu_baseline(x, L, sample, threads, eps, gpu_q):
@@ -106,13 +109,12 @@ def main():
 
     def step():
         ss.reset()
-        ss.ingest(x, offs)
-        return ss.quantiles(qs)
+        # add every value, then quantiles(qs) -- one fused pass (gk_ingest_quantiles)
+        return ss.ingest(x, offs, quantiles=qs)
 
-    # algorithmic bytes of one k_ingest launch (untimed)
-    ss.reset()
-    ss.ingest(x, offs)
-    bytes_per_launch = algorithmic_bytes(ss, S, N)
+    # algorithmic bytes of one k_ingest launch (untimed identical step)
+    step()
+    bytes_per_launch = algorithmic_bytes(ss, S, N, len(qs))
 
     for _ in range(a.warmup):
         step()

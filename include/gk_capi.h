@@ -81,6 +81,13 @@ int gk_flush(gk_set* set, void* stream);
 int gk_quantiles(gk_set* set, const double* qs, int nq, double* out, int mode,
                  void* stream);
 
+/* gk_ingest followed by gk_quantiles, fused: every stream adds its values
+ * (gk:49-61), then answers quantiles(qs) (gk:187-232) -- the leftover pending
+ * values are flushed first, as the reference does -- from the table while it
+ * is still on chip.  Same arguments and semantics as the two calls. */
+int gk_ingest_quantiles(gk_set* set, const double* values, const int64_t* offsets,
+                        const double* qs, int nq, double* out, int mode, void* stream);
+
 /* Per-stream accessors num_values/_min/_max/sum/avg (gk:35-42, 25-29) and the
  * table size len(entries) / pending count len(incoming) WITHOUT flushing.
  * Any pointer may be NULL.  All outputs are device arrays of length S. */

@@ -210,25 +210,26 @@ int check_set(const gk_set* h) {
 }
 
 hipError_t launch_class(gk_set* h, int c, const double* x, const int64_t* offs, const int32_t* list, int64_t count,
-                        int force, hipStream_t stream) {
+                        int force, const GKQuery& q, hipStream_t stream) {
   return gk_launch_ingest(h->st.cap[c], h->vpl, h->st, x, offs, list, count, force, h->d_ws, h->ws_bytes,
-                          h->ws_blocks, h->d_ovf_count, h->d_ovf_list, stream);
+                          h->ws_blocks, h->d_ovf_count, h->d_ovf_list, q, stream);
 }
 
 // Launch the ingest/flush kernel over every stream (class 0 over all, each
 // larger class over its member list); streams that overflow their class were
 // not committed, so they are promoted one class up and run again.
-int run_ingest(gk_set* h, const double* x, const int64_t* offs, int force, hipStream_t stream) {
+int run_ingest(gk_set* h, const double* x, const int64_t* offs, int force, hipStream_t stream,
+               const GKQuery& q = GKQuery()) {
   if (!offs) offs = h->d_zero_offs;
   HIP_TRY(hipMemsetAsync(h->d_ovf_count, 0, sizeof(int32_t), stream));
   // timing covers the class-0 batch launch of gk_ingest (force == 0) only
-  const bool timed = h->timing && force == 0;
+  const bool timed = h->timing && x != nullptr;
   if (timed) HIP_TRY(hipEventRecord(h->ev[0], stream));
-  HIP_TRY(launch_class(h, 0, x, offs, nullptr, h->S, force, stream));
+  HIP_TRY(launch_class(h, 0, x, offs, nullptr, h->S, force, q, stream));
   if (timed) HIP_TRY(hipEventRecord(h->ev[1], stream));
   for (int c = 1; c < h->st.nclass; ++c)
     if (!h->members[c].empty())
-      HIP_TRY(launch_class(h, c, x, offs, h->d_list[c], (int64_t)h->members[c].size(), force, stream));
+      HIP_TRY(launch_class(h, c, x, offs, h->d_list[c], (int64_t)h->members[c].size(), force, q, stream));
   std::vector<int32_t> ovf;
   int64_t cnt = read_overflow(h, ovf, stream);
   if (cnt < 0) return (int)cnt;
@@ -255,7 +256,7 @@ int run_ingest(gk_set* h, const double* x, const int64_t* offs, int force, hipSt
       if (rc) return rc;
       HIP_TRY(hipMemcpyAsync(h->d_tmp_list, by[c].data(), by[c].size() * sizeof(int32_t), hipMemcpyHostToDevice,
                              stream));
-      HIP_TRY(launch_class(h, c, x, offs, h->d_tmp_list, (int64_t)by[c].size(), force, stream));
+      HIP_TRY(launch_class(h, c, x, offs, h->d_tmp_list, (int64_t)by[c].size(), force, q, stream));
       HIP_TRY(hipStreamSynchronize(stream));
     }
     cnt = read_overflow(h, ovf, stream);
@@ -459,18 +460,12 @@ int gk_flush(gk_set* h, void* stream) {
   return run_ingest(h, nullptr, nullptr, 1, (hipStream_t)stream);
 }
 
-int gk_quantiles(gk_set* h, const double* qs, int nq, double* out, int mode, void* stream) {
-  int rc = check_set(h);
-  if (rc) return rc;
+// quantile arguments -> device copy of qs and the effective mode
+static int prepare_query(gk_set* h, const double* qs, int nq, double* out, int mode, hipStream_t s, GKQuery* q) {
   if (nq < 0 || (nq > 0 && (!qs || !out))) return fail(GK_E_ARG, "bad quantile arguments");
   if (mode != GK_Q_LIST && mode != GK_Q_SINGLE) return fail(GK_E_ARG, "bad mode %d", mode);
   for (int i = 0; i < nq; ++i)
     if (std::isnan(qs[i])) return fail(GK_E_ARG, "cannot convert float NaN to integer");
-  if (nq == 0 || h->S == 0) return GK_OK;
-  hipStream_t s = (hipStream_t)stream;
-  // gk:197-198: pending values are flushed first (state mutation)
-  rc = run_ingest(h, nullptr, nullptr, 1, s);
-  if (rc) return rc;
   // gk:205-206: an unsorted list is answered q by q with quantile()
   int eff_mode = mode;
   if (mode == GK_Q_LIST) {
@@ -487,8 +482,54 @@ int gk_quantiles(gk_set* h, const double* qs, int nq, double* out, int mode, voi
     if (hipMalloc(&h->d_qs, cap * sizeof(double)) != hipSuccess) return fail(GK_E_NOMEM, "qs allocation failed");
     h->qs_alloc = cap;
   }
-  HIP_TRY(hipMemcpyAsync(h->d_qs, qs, nq * sizeof(double), hipMemcpyHostToDevice, s));
-  HIP_TRY(gk_launch_quantiles(h->st, h->d_qs, nq, out, eff_mode, s));
+  if (nq) HIP_TRY(hipMemcpyAsync(h->d_qs, qs, nq * sizeof(double), hipMemcpyHostToDevice, s));
+  q->qs = nq ? h->d_qs : nullptr;
+  q->nq = nq;
+  q->out = out;
+  q->mode = eff_mode;
+  return GK_OK;
+}
+
+int gk_quantiles(gk_set* h, const double* qs, int nq, double* out, int mode, void* stream) {
+  int rc = check_set(h);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  GKQuery q;
+  rc = prepare_query(h, qs, nq, out, mode, s, &q);
+  if (rc) return rc;
+  if (nq == 0 || h->S == 0) return GK_OK;
+  // gk:197-198: pending values are flushed first (state mutation); the
+  // quantiles are answered in the same launch from the flushed table
+  rc = run_ingest(h, nullptr, nullptr, 1, s, q);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(s));
+  return GK_OK;
+}
+
+int gk_ingest_quantiles(gk_set* h, const double* values, const int64_t* offsets, const double* qs, int nq,
+                        double* out, int mode, void* stream) {
+  int rc = check_set(h);
+  if (rc) return rc;
+  if (!offsets) return fail(GK_E_ARG, "offsets is null");
+  if (!values) return fail(GK_E_ARG, "values is null");
+  hipStream_t s = (hipStream_t)stream;
+  GKQuery q;
+  rc = prepare_query(h, qs, nq, out, mode, s, &q);
+  if (rc) return rc;
+  if (h->S == 0) return GK_OK;
+  if (nq == 0) return gk_ingest(h, values, offsets, stream);
+  if (h->timing) HIP_TRY(hipEventRecord(h->ev[2], s));
+  HIP_TRY(gk_launch_stats(h->st, values, offsets, s));
+  if (h->timing) HIP_TRY(hipEventRecord(h->ev[3], s));
+  // add every value (gk:49-61), then quantiles() (gk:187-232): flush the
+  // leftover pending values and answer from the LDS-resident table
+  rc = run_ingest(h, values, offsets, 1, s, q);
+  if (rc) return rc;
+  if (h->timing) {
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, h->ev[2], h->ev[3]));
+    h->stats_ms += ms;
+  }
   HIP_TRY(hipStreamSynchronize(s));
   return GK_OK;
 }

@@ -10,8 +10,9 @@
 //   k_ingest     gk:60-109  wave per stream: flush schedule + closed-form
 //                           merge_compress of each flush, table kept in LDS
 //                           for the whole call
-//   k_quantiles  gk:156-232 wave per stream: rank walk as a count over the
-//                           running max of prefix(g)+delta; small-n percentile
+//                           + optional fused quantiles (gk:156-232) answered
+//                           from the LDS table after the final flush: rank walk
+//                           as a count over the running max of prefix(g)+delta
 //   k_merge      gk:111-154 wave per stream: convert `other`, stable merge of
 //                           the incoming list, general four-rule walk (gk:76-106)
 //   k_export / k_import / k_reset: state movement
@@ -140,6 +141,7 @@ __device__ __forceinline__ void gk_load_flush_values(double (&xv)[VPL], const do
 struct GKHdrV {
   int32_t cls, slot, pend, E;
   int64_t n, xo, xe;
+  double mn, mx;
 };
 
 __device__ __forceinline__ void gk_hdr_issue(GKHdrV& h, const GKState& st, const int64_t* offs, int64_t s) {
@@ -150,6 +152,8 @@ __device__ __forceinline__ void gk_hdr_issue(GKHdrV& h, const GKState& st, const
   h.n = st.n[s];
   h.xo = offs[s];
   h.xe = offs[s + 1];
+  h.mn = st.mn[s];
+  h.mx = st.mx[s];
 }
 
 __device__ __forceinline__ int64_t rfl64(int64_t v) {
@@ -207,18 +211,29 @@ __global__ __launch_bounds__(256) void k_stats(GKState st, const double* __restr
     av = st.avg[s];
   }
   const int sub = t & 15;   // lane within a stream's 16-lane group
-  const int grp = t >> 4;   // 16 streams per pass
+  const int grp = t >> 4;   // 16 streams per load row
+  // this thread's 16 load slots: stream r*16+grp, value k0+sub (bounds read
+  // from LDS each time: keeping them in registers costs 64 VGPRs)
+  // chunk k0's values are loaded into registers while chunk k0-16 is walked
+  double rv[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int ls = min(r * 16 + grp, nstr);
+    const int64_t i = so[ls] + sub;
+    rv[r] = (i < so[min(ls + 1, nstr)]) ? x[i] : 0.0;
+  }
   for (int64_t k0 = 0; k0 < maxL; k0 += STATS_CHUNK) {
-#pragma unroll 4
-    for (int r = 0; r < 16; ++r) {
-      const int ls = r * 16 + grp;
-      if (ls < nstr) {
-        const int64_t o = so[ls], e = so[ls + 1];
-        const int64_t i = o + k0 + sub;
-        tile[ls * STATS_ROW + sub] = (i < e) ? x[i] : 0.0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) tile[(r * 16 + grp) * STATS_ROW + sub] = rv[r];
+    __syncthreads();
+    if (k0 + STATS_CHUNK < maxL) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ls = min(r * 16 + grp, nstr);
+        const int64_t i = so[ls] + k0 + STATS_CHUNK + sub;
+        rv[r] = (i < so[min(ls + 1, nstr)]) ? x[i] : 0.0;
       }
     }
-    __syncthreads();
     if (t < nstr) {
       const int kmax = (int)min((int64_t)STATS_CHUNK, L - k0);
       for (int k = 0; k < kmax; ++k) {
@@ -674,6 +689,102 @@ __device__ __forceinline__ int flush_wave(const FlushBuf& L, const int cap, cons
   return newE;
 }
 
+
+// ===========================================================================
+// Quantiles of one stream from its table (gk:156-232), wave-parallel.
+//   large n: the reference walks i = 0.. while prefix_g(i) + d_i - 1 <=
+//   rank + spread; the first i that breaks is the number of i whose RUNNING
+//   MAX of prefix_g + d - 1 is <= rank + spread (the running max is
+//   monotone), so each q is one count over the table.
+//   small n (n < 1/eps, gk:169): numpy.percentile(values, q*100), linear.
+// qmode 0 (quantiles, sorted qs): no break -> _max (gk:225-230)
+// qmode 1 (quantile / unsorted qs): no break -> entries[-1].val (gk:185)
+// ===========================================================================
+__device__ __forceinline__ double gk_nan() { return __longlong_as_double(0x7ff8000000000000LL); }
+
+__device__ double percentile_linear_arr(const double* __restrict__ tv, int E, double q) {
+  // numpy 2.2.6 _function_base_impl.py: q/100 (l.4257), (n-1)*q (l.107),
+  // bounds (l.4748-4750), gamma (l.4632), _lerp (l.4653-4657)
+  const double qq = (q * 100.0) / 100.0;
+  const double vi = (double)(E - 1) * qq;
+  double prev;
+  double a, b;
+  if (vi >= (double)(E - 1)) {
+    prev = -1.0;
+    a = tv[E - 1];
+    b = a;
+  } else if (vi < 0.0) {
+    prev = 0.0;
+    a = tv[0];
+    b = a;
+  } else {
+    prev = floor(vi);
+    const int pi = (int)prev;
+    a = tv[pi];
+    b = tv[pi + 1];
+  }
+  const double gamma = vi - prev;
+  const double diff = b - a;
+  if (gamma >= 0.5) return b - diff * (1.0 - gamma);
+  return a + diff * gamma;
+}
+
+__device__ __attribute__((noinline)) void wave_quantiles(const double* __restrict__ tv, const int32_t* __restrict__ tg,
+                               const int32_t* __restrict__ td, int E, int64_t n, double mn, double mx,
+                               const GKState& st, const double* __restrict__ qs, int nq, int qmode,
+                               double* __restrict__ out, int lane) {
+  if (n == 0 || E == 0) {
+    for (int q = lane; q < nq; q += 64) out[q] = gk_nan();
+    return;
+  }
+  if ((double)n < st.inv_eps) {  // gk:169 / gk:200
+    for (int q = lane; q < nq; q += 64) {
+      const double qv = qs[q];
+      out[q] = (qv >= 0.0 && qv <= 1.0) ? percentile_linear_arr(tv, E, qv) : gk_nan();
+    }
+    return;
+  }
+  const int K = (E + 63) >> 6;
+  const int j0 = lane * K;
+  const int jend = min(j0 + K, E);
+  int64_t bsum = 0;
+  for (int j = j0; j < jend; ++j) bsum += tg[j];
+  const int64_t bex = wave_incl_scan_i64(bsum, lane) - bsum;
+  int64_t acc = bex, bmax = INT64_MIN;
+  for (int j = j0; j < jend; ++j) {
+    acc += tg[j];
+    const int64_t a = acc + td[j] - 1;
+    if (a > bmax) bmax = a;
+  }
+  const int64_t pmax_incl = wave_incl_max_i64(bmax, lane);
+  int64_t pmax_ex = __shfl_up(pmax_incl, 1, 64);
+  if (lane == 0) pmax_ex = INT64_MIN;
+  const int64_t spread = (int64_t)(st.eps * (double)(n - 1));  // gk:174 / gk:210
+  for (int q = 0; q < nq; ++q) {
+    const double qv = qs[q];
+    const bool valid = (qv >= 0.0 && qv <= 1.0);
+    const int64_t rank = valid ? (int64_t)(qv * (double)(n - 1) + 1.0) : 0;  // gk:173
+    const int64_t th = rank + spread;
+    int c = 0;
+    int64_t run = pmax_ex, a2 = bex;
+    for (int j = j0; j < jend; ++j) {
+      a2 += tg[j];
+      const int64_t a = a2 + td[j] - 1;
+      if (a > run) run = a;
+      c += (run <= th) ? 1 : 0;
+    }
+    const int i = wave_sum_i32(c);
+    if (lane == 0) {
+      double r;
+      if (!valid) r = gk_nan();
+      else if (i == 0) r = mn;                          // gk:182-183 / gk:220
+      else if (i < E) r = tv[i - 1];                    // gk:185 / gk:220
+      else r = (qmode == 0) ? mx : tv[E - 1];           // gk:229 / gk:185
+      out[q] = r;
+    }
+  }
+}
+
 // CAP > 0: LDS working storage of that capacity (class 256 / 2048).
 // CAP == 0: global workspace `ws` (ws_bytes per block) of capacity `cap`.
 // list == NULL: every class-0 stream; else the listed streams (class c > 0).
@@ -683,7 +794,8 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
                                                const int32_t* __restrict__ list, int64_t count,
                                                int force, int cap, unsigned char* ws, size_t ws_bytes,
                                                int32_t* __restrict__ ovf_count,
-                                               int32_t* __restrict__ ovf_list) {
+                                               int32_t* __restrict__ ovf_list, const double* __restrict__ qs,
+                                               int nq, double* __restrict__ qout, int qmode) {
   constexpr int LCAP = CAP > 0 ? CAP : 1;
   constexpr int LVPL = CAP > 0 ? VPL : 1;
   constexpr int KMAX = CAP == 256 ? 4 : 0;  // registers cache a lane's block of entries
@@ -711,13 +823,16 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
     int64_t n = rfl64(hv.n);
     const int64_t xo = rfl64(hv.xo);
     const int64_t xe = rfl64(hv.xe);
+    const double smn = __longlong_as_double(rfl64(__double_as_longlong(hv.mn)));
+    const double smx = __longlong_as_double(rfl64(__double_as_longlong(hv.mx)));
     if (w + G < count) gk_hdr_issue(hv, st, offs, list ? (int64_t)list[w + G] : w + G);
     if (!list && scls != 0) continue;  // promoted: handled by its class launch
     const int64_t Lx = xe - xo;
 
     // force 1: flush only if values are pending (size/quantile, gk:45, 166, 197)
     // force 2: unconditional merge_compress() (merge, gk:122, 126, 137)
-    if (Lx <= 0 && !((force == 1 && p > 0) || (force == 2 && n > 0))) continue;
+    // a query launch (qs != NULL, force 1) answers every stream
+    if (Lx <= 0 && !((force == 1 && p > 0) || (force == 2 && n > 0)) && !qs) continue;
     GKRec* __restrict__ tab = gk_table_ptr_cs(st, s, scls, sslot);
     double* __restrict__ pb = st.pbuf + s * (int64_t)st.pmax;
     int cur = 0;
@@ -824,6 +939,7 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
       const double* fv = cur ? B.tv[1] : B.tv[0];
       const int32_t* fg = cur ? B.tg[1] : B.tg[0];
       const int32_t* fd = cur ? B.td[1] : B.td[0];
+      if (qs) wave_quantiles(fv, fg, fd, E, n, smn, smx, st, qs, nq, qmode, qout + s * (int64_t)nq, lane);
       for (int j = lane; j < E; j += 64) {
         GKRec rc;
         rc.v = fv[j];
@@ -838,110 +954,6 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
       st.pend[s] = p;
     }
     wsync<CAP == 0>();
-  }
-}
-
-// ===========================================================================
-// k_quantiles: gk:156-232.  One wave per stream, table read straight from HBM.
-//   large n: the reference walks i = 0.. while prefix_g(i) + d_i - 1 <= rank
-//   + spread.  The first i that breaks is the number of i whose RUNNING MAX
-//   of prefix_g + d - 1 is <= rank + spread (the running max is monotone),
-//   so each q is one count over the table.
-//   small n (n < 1/eps, gk:169): numpy.percentile(values, q*100), linear.
-// mode 0 (quantiles, sorted qs): no break -> _max (gk:225-230)
-// mode 1 (quantile / unsorted qs): no break -> entries[-1].val (gk:185)
-// ===========================================================================
-__device__ __forceinline__ double gk_nan() { return __longlong_as_double(0x7ff8000000000000LL); }
-
-__device__ double percentile_linear(const GKRec* __restrict__ tab, int E, double q) {
-  // numpy 2.2.6 _function_base_impl.py: q/100 (l.4257), (n-1)*q (l.107),
-  // bounds (l.4748-4750), gamma (l.4632), _lerp (l.4653-4657)
-  const double qq = (q * 100.0) / 100.0;
-  const double vi = (double)(E - 1) * qq;
-  double prev;
-  double a, b;
-  if (vi >= (double)(E - 1)) {
-    prev = -1.0;
-    a = tab[E - 1].v;
-    b = a;
-  } else if (vi < 0.0) {
-    prev = 0.0;
-    a = tab[0].v;
-    b = a;
-  } else {
-    prev = floor(vi);
-    const int pi = (int)prev;
-    a = tab[pi].v;
-    b = tab[pi + 1].v;
-  }
-  const double gamma = vi - prev;
-  const double diff = b - a;
-  if (gamma >= 0.5) return b - diff * (1.0 - gamma);
-  return a + diff * gamma;
-}
-
-__global__ __launch_bounds__(64) void k_quantiles(GKState st, const double* __restrict__ qs, int nq,
-                                                  double* __restrict__ out, int mode) {
-  const int lane = threadIdx.x;
-  for (int64_t s = blockIdx.x; s < st.S; s += gridDim.x) {
-    double* o = out + s * (int64_t)nq;
-    const int64_t n = st.n[s];
-    const int E = st.E[s];
-    if (n == 0 || E == 0) {
-      for (int q = lane; q < nq; q += 64) o[q] = gk_nan();
-      continue;
-    }
-    const GKRec* __restrict__ tab = gk_table_ptr(st, s);
-    const double mn = st.mn[s], mx = st.mx[s];
-    if ((double)n < st.inv_eps) {  // gk:169 / gk:200
-      for (int q = lane; q < nq; q += 64) {
-        const double qv = qs[q];
-        o[q] = (qv >= 0.0 && qv <= 1.0) ? percentile_linear(tab, E, qv) : gk_nan();
-      }
-      continue;
-    }
-    const int K = (E + 63) >> 6;
-    const int j0 = lane * K;
-    const int jend = min(j0 + K, E);
-    int64_t bsum = 0;
-    for (int j = j0; j < jend; ++j) bsum += tab[j].g;
-    const int64_t bex = wave_incl_scan_i64(bsum, lane) - bsum;
-    // running max of prefix_g(i) + d_i - 1, block-local then across lanes
-    int64_t acc = bex, bmax = INT64_MIN;
-    for (int j = j0; j < jend; ++j) {
-      const GKRec rc = tab[j];
-      acc += rc.g;
-      const int64_t a = acc + rc.d - 1;
-      if (a > bmax) bmax = a;
-    }
-    const int64_t pmax_incl = wave_incl_max_i64(bmax, lane);
-    int64_t pmax_ex = __shfl_up(pmax_incl, 1, 64);
-    if (lane == 0) pmax_ex = INT64_MIN;
-    const int64_t spread = (int64_t)(st.eps * (double)(n - 1));  // gk:174 / gk:210
-    for (int q = 0; q < nq; ++q) {
-      const double qv = qs[q];
-      const bool valid = (qv >= 0.0 && qv <= 1.0);
-      const int64_t rank = valid ? (int64_t)(qv * (double)(n - 1) + 1.0) : 0;  // gk:173
-      const int64_t th = rank + spread;
-      int c = 0;
-      int64_t run = pmax_ex, a2 = bex;
-      for (int j = j0; j < jend; ++j) {
-        const GKRec rc = tab[j];
-        a2 += rc.g;
-        const int64_t a = a2 + rc.d - 1;
-        if (a > run) run = a;
-        c += (run <= th) ? 1 : 0;
-      }
-      const int i = wave_sum_i32(c);
-      if (lane == 0) {
-        double r;
-        if (!valid) r = gk_nan();
-        else if (i == 0) r = mn;                         // gk:182-183 / gk:220
-        else if (i < E) r = tab[i - 1].v;                // gk:185 / gk:220
-        else r = (mode == 0) ? mx : tab[E - 1].v;        // gk:229 / gk:185
-        o[q] = r;
-      }
-    }
   }
 }
 
@@ -1346,7 +1358,7 @@ template <int CAP, int VPL>
 static hipError_t launch_ingest_t(const GKState& st, const double* x, const int64_t* offs,
                                   const int32_t* list, int64_t count, int force, int cap,
                                   unsigned char* ws, size_t ws_bytes, int64_t ws_blocks,
-                                  int32_t* ovf_count, int32_t* ovf_list, hipStream_t stream) {
+                                  int32_t* ovf_count, int32_t* ovf_list, const GKQuery& q, hipStream_t stream) {
   if (count <= 0) return hipSuccess;
   int64_t grid;
   if (CAP > 0) {
@@ -1360,7 +1372,7 @@ static hipError_t launch_ingest_t(const GKState& st, const double* x, const int6
   if (grid > count) grid = count;
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL((k_ingest<CAP, VPL>), dim3((unsigned)grid), dim3(64), 0, stream, st, x, offs, list,
-                     count, force, cap, ws, ws_bytes, ovf_count, ovf_list);
+                     count, force, cap, ws, ws_bytes, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode);
   return hipGetLastError();
 }
 
@@ -1368,9 +1380,9 @@ template <int CAP>
 static hipError_t launch_ingest_vpl(int vpl, const GKState& st, const double* x, const int64_t* offs,
                                     const int32_t* list, int64_t count, int force, int cap, unsigned char* ws,
                                     size_t ws_bytes, int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list,
-                                    hipStream_t stream) {
+                                    const GKQuery& q, hipStream_t stream) {
 #define GK_L(V) launch_ingest_t<CAP, V>(st, x, offs, list, count, force, cap, ws, ws_bytes, ws_blocks, \
-                                        ovf_count, ovf_list, stream)
+                                        ovf_count, ovf_list, q, stream)
   switch (vpl) {
     case 1: return GK_L(1);
     case 2: return GK_L(2);
@@ -1386,18 +1398,19 @@ size_t gk_ingest_ws_bytes(int cap, int vpl) { return gk_flush_ws_bytes(cap, vpl)
 
 hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x, const int64_t* offs,
                             const int32_t* list, int64_t count, int force, unsigned char* ws, size_t ws_bytes,
-                            int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list, hipStream_t stream) {
+                            int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list, const GKQuery& q,
+                            hipStream_t stream) {
   switch (cap) {
     case 256:
       return launch_ingest_vpl<256>(vpl, st, x, offs, list, count, force, cap, nullptr, 0, 0, ovf_count, ovf_list,
-                                    stream);
+                                    q, stream);
     case 2048:
       return launch_ingest_vpl<2048>(vpl, st, x, offs, list, count, force, cap, nullptr, 0, 0, ovf_count, ovf_list,
-                                     stream);
+                                     q, stream);
     default:
       if (!ws || ws_blocks <= 0) return hipErrorInvalidValue;
       return launch_ingest_vpl<0>(vpl, st, x, offs, list, count, force, cap, ws, ws_bytes, ws_blocks, ovf_count,
-                                  ovf_list, stream);
+                                  ovf_list, q, stream);
   }
 }
 
@@ -1405,15 +1418,6 @@ hipError_t gk_launch_stats(const GKState& st, const double* x, const int64_t* of
   if (st.S <= 0) return hipSuccess;
   const int64_t grid = (st.S + 255) / 256;
   hipLaunchKernelGGL(k_stats, dim3((unsigned)grid), dim3(256), 0, stream, st, x, offs);
-  return hipGetLastError();
-}
-
-hipError_t gk_launch_quantiles(const GKState& st, const double* qs, int nq, double* out, int mode,
-                               hipStream_t stream) {
-  if (st.S <= 0) return hipSuccess;
-  int64_t grid = (int64_t)num_cu() * 32;
-  if (grid > st.S) grid = st.S;
-  hipLaunchKernelGGL(k_quantiles, dim3((unsigned)grid), dim3(64), 0, stream, st, qs, nq, out, mode);
   return hipGetLastError();
 }
 

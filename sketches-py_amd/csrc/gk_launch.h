@@ -7,6 +7,14 @@
 
 #include "gk_state.h"
 
+// optional query fused into an ingest/flush launch (gk:187-232 after the flush)
+struct GKQuery {
+  const double* qs = nullptr;  // device, nq values (NULL: no query)
+  int nq = 0;
+  double* out = nullptr;       // device [S * nq]
+  int mode = 0;                // 0 quantiles() list semantics, 1 quantile() per q
+};
+
 struct MergeArgsHost {
   GKState dst;
   GKState src;
@@ -30,10 +38,9 @@ size_t gk_ingest_ws_bytes(int cap, int vpl);
 // cap 256 / 2048: LDS kernels; any other cap: global workspace ws (ws_bytes per block, ws_blocks blocks)
 hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x, const int64_t* offs,
                             const int32_t* list, int64_t count, int force, unsigned char* ws, size_t ws_bytes,
-                            int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list, hipStream_t stream);
+                            int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list, const GKQuery& q,
+                            hipStream_t stream);
 hipError_t gk_launch_stats(const GKState& st, const double* x, const int64_t* offs, hipStream_t stream);
-hipError_t gk_launch_quantiles(const GKState& st, const double* qs, int nq, double* out, int mode,
-                               hipStream_t stream);
 size_t gk_merge_lds_bytes(int cap, int pmax);
 hipError_t gk_launch_merge(const MergeArgsHost& h, hipStream_t stream);
 hipError_t gk_launch_reset(const GKState& st, hipStream_t stream);

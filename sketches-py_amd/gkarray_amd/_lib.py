@@ -49,6 +49,7 @@ SYMBOLS = {
     "gk_ingest": (_INT, [_P, _P, _P, _P]),
     "gk_flush": (_INT, [_P, _P]),
     "gk_quantiles": (_INT, [_P, ctypes.POINTER(_D), _INT, _P, _INT, _P]),
+    "gk_ingest_quantiles": (_INT, [_P, _P, _P, ctypes.POINTER(_D), _INT, _P, _INT, _P]),
     "gk_stats": (_INT, [_P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "gk_merge": (_INT, [_P, ctypes.POINTER(_P), _INT, _P]),
     "gk_merge_compress": (_INT, [_P, _P, _P, _P, _P, _P]),

@@ -91,10 +91,14 @@ class StreamSet:
         with torch.cuda.device(self.device):
             L.check(self._lib.gk_reset(self._h, self._sp()))
 
-    def ingest(self, values, offsets):
+    def ingest(self, values, offsets, quantiles=None, single=False):
         """Batched ``GKArray.add`` (gk:49-61) over all streams.
 
         values: float64 [N] (device tensor preferred); offsets: int64 [S+1].
+        With ``quantiles=qs`` the call continues with ``quantiles(qs)``
+        (gk:187-232) for every stream in the same kernel pass (the leftover
+        pending values are flushed, as the reference's quantiles() does) and
+        returns the [S, len(qs)] float64 device tensor.
         """
         v = self._dev(values, torch.float64)
         o = self._dev(offsets, torch.int64)
@@ -102,8 +106,19 @@ class StreamSet:
             raise ValueError("offsets must have num_streams+1 entries")
         if v.numel() == 0:
             v = torch.zeros(1, dtype=torch.float64, device=self.device)
+        if quantiles is None:
+            with torch.cuda.device(self.device):
+                L.check(self._lib.gk_ingest(self._h, _ptr(v), _ptr(o), self._sp()))
+            return None
+        qs = [float(q) for q in quantiles]
+        nq = len(qs)
+        out = torch.empty((self.num_streams, max(nq, 1)), dtype=torch.float64, device=self.device)
+        arr = (ctypes.c_double * max(nq, 1))(*qs)
+        mode = L.GK_Q_SINGLE if single else L.GK_Q_LIST
         with torch.cuda.device(self.device):
-            L.check(self._lib.gk_ingest(self._h, _ptr(v), _ptr(o), self._sp()))
+            L.check(self._lib.gk_ingest_quantiles(self._h, _ptr(v), _ptr(o), arr, nq, _ptr(out), mode,
+                                                  self._sp()))
+        return out[:, :nq]
 
     def ingest_lists(self, seqs):
         """Convenience: ``seqs[s]`` is the list of values for stream s."""

@@ -33,16 +33,21 @@ def resource_report(tmp_path_factory):
     return kernels
 
 
-def test_ingest_kernels_do_not_spill(resource_report):
-    """k_ingest issues asm loads whose registers are waited for explicitly
-    (gk_load_async / gk_vm_wait); a VGPR spill would read such a register
-    before its load lands.  Every k_ingest instantiation must have zero
-    scratch."""
-    ingest = {k: v for k, v in resource_report.items() if "k_ingest" in k}
-    assert len(ingest) >= 10
-    bad = {k: v.get("ScratchSize [bytes/lane]") for k, v in ingest.items()
-           if v.get("ScratchSize [bytes/lane]", 0) != 0 or v.get("VGPRs Spill", 0) != 0}
+def test_fast_class_has_no_scratch(resource_report):
+    """The 256-entry class runs nearly every stream: no scratch traffic."""
+    fast = {k: v for k, v in resource_report.items() if k.startswith("_Z8k_ingestILi256E")}
+    assert len(fast) == 5
+    bad = {k: v.get("ScratchSize [bytes/lane]") for k, v in fast.items() if v.get("ScratchSize [bytes/lane]", 0)}
     assert not bad, bad
+
+
+def test_no_inline_asm_memory_ops():
+    """Inline-asm loads were rejected: the compiler may copy an asm output
+    register before the load lands (tools/check_async_loads.py found such
+    copies).  Memory operations in the kernels stay compiler-visible."""
+    src = open(os.path.join(CSRC, "gk_kernels.hip")).read()
+    for m in re.finditer(r'asm\s+volatile\s*\(\s*"([^"]*)"', src):
+        assert "load" not in m.group(1) and "store" not in m.group(1), m.group(1)
 
 
 def test_fast_class_occupancy(resource_report):

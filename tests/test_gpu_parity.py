@@ -358,3 +358,23 @@ def test_large_batch_properties_and_sample(gpu_device):
         assert np.array_equal(gv[a:b].view(np.int64), ov[oo[k]:oo[k + 1]].view(np.int64))
         assert np.array_equal(ggn[a:b].astype(np.int64), og[oo[k]:oo[k + 1]])
         assert np.array_equal(gdn[a:b].astype(np.int64), od[oo[k]:oo[k + 1]])
+
+
+def test_fused_ingest_quantiles_vs_oracle(gpu_device):
+    """gk_ingest_quantiles == gk_ingest then gk_quantiles (state and answers)."""
+    rng = np.random.default_rng(31)
+    for eps in (0.05, 0.01):
+        S = 700
+        P = int(1.0 / eps) + 1
+        lens = rng.integers(0, 9 * P, S)
+        lens[:3] = [0, 1, P]
+        seqs = [gen(int(d), int(L), rng) for d, L in zip(rng.integers(0, 8, S), lens)]
+        flat, offs = csr(seqs)
+        ss = _ss(S, eps, gpu_device)
+        osx = OracleSet(S, eps)
+        for qs, single in (([0.5, 0.9, 0.99], False), ([0.99, 0.1], False), ([0.0, 1.0, 2.0], True)):
+            got = ss.ingest(torch.from_numpy(flat), torch.from_numpy(offs), quantiles=qs, single=single)
+            osx.ingest(flat, offs)
+            exp = osx.quantiles(qs, single=single)
+            assert_same_quantiles(got.cpu().numpy(), exp, "fused eps=%g qs=%r" % (eps, qs))
+            assert_same_state(ss, osx, "fused state eps=%g" % eps)
