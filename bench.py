@@ -38,23 +38,30 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--streams", type=int, default=1_000_000, help="streams per GPU")
-    ap.add_argument("--values", type=int, default=1000, help="values per stream")
+    ap.add_argument("--workload", default="cfg3", choices=["cfg3", "cfg2", "cfg4"],
+                    help="cfg3 (default, the metric's config): 1M streams x 1k Pareto values per GPU; "
+                         "cfg2: 100k x 10k lognormal; cfg4: 10k streams x 1M lognormal values "
+                         "row-sharded over the GPUs, merged by all-gather + rank-ordered fold")
+    ap.add_argument("--streams", type=int, default=None, help="override: streams per GPU (cfg4: total)")
+    ap.add_argument("--values", type=int, default=None, help="override: values per stream (cfg4: total)")
     ap.add_argument("--eps", type=float, default=0.01)
     ap.add_argument("--seed", type=int, default=3)
-    ap.add_argument("--cpu-sample", type=int, default=100000,
+    ap.add_argument("--cpu-sample", type=int, default=300000,
                     help="streams of the same workload timed on the host oracle (rank 0, N=1)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, os.cpu_count())")
     ap.add_argument("--no-cpu", action="store_true")
     return ap.parse_args()
 
 
-def make_input(S, L, seed, device):
+def make_input(S, L, seed, device, dist_name="pareto"):
     g = torch.Generator(device=device)
     g.manual_seed(seed)
-    u = torch.rand(S * L, dtype=torch.float64, device=device, generator=g)
-    x = (1.0 - u).pow_(-1.0 / 1.5)  # numpy pareto(1.5) + 1 by inversion
-    del u
+    if dist_name == "pareto":
+        u = torch.rand(S * L, dtype=torch.float64, device=device, generator=g)
+        x = (1.0 - u).pow_(-1.0 / 1.5)  # numpy pareto(1.5) + 1 by inversion
+        del u
+    else:  # lognormal(0, 1)
+        x = torch.randn(S * L, dtype=torch.float64, device=device, generator=g).exp_()
     offs = torch.arange(0, S * L + 1, L, dtype=torch.int64, device=device)
     return x, offs
 
@@ -101,20 +108,41 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
     from gkarray_amd import StreamSet
 
-    S, L = a.streams, a.values
-    N = S * L
-    x, offs = make_input(S, L, a.seed + rank, dev)
-    ss = StreamSet(S, a.eps, device=dev)
+    defaults = {"cfg3": (1_000_000, 1000, "pareto"), "cfg2": (100_000, 10_000, "lognormal"),
+                "cfg4": (10_000, 1_000_000, "lognormal")}
+    S, L, dist_name = defaults[a.workload]
+    S = a.streams or S
+    L = a.values or L
     qs = [0.5, 0.9, 0.99]
+    if a.workload == "cfg4":
+        # rows of every stream split over the ranks: this rank sketches its
+        # L/world values of each of the S streams, then the shards are merged
+        from gkarray_amd import dist as gd
+        L = L // world
+        N = S * L
+        x, offs = make_input(S, L, a.seed + rank, dev, dist_name)
+        ss = StreamSet(S, a.eps, device=dev)
 
-    def step():
-        ss.reset()
-        # add every value, then quantiles(qs) -- one fused pass (gk_ingest_quantiles)
-        return ss.ingest(x, offs, quantiles=qs)
+        def step():
+            ss.reset()
+            ss.ingest(x, offs)
+            merged, _ = gd.merge_row_shards(ss)
+            q = merged.quantiles(qs)
+            merged.close()
+            return q
+    else:
+        N = S * L
+        x, offs = make_input(S, L, a.seed + rank, dev, dist_name)
+        ss = StreamSet(S, a.eps, device=dev)
+
+        def step():
+            ss.reset()
+            # add every value, then quantiles(qs) -- one fused pass (gk_ingest_quantiles)
+            return ss.ingest(x, offs, quantiles=qs)
 
     # algorithmic bytes of one k_ingest launch (untimed identical step)
     step()
-    bytes_per_launch = algorithmic_bytes(ss, S, N, len(qs))
+    bytes_per_launch = algorithmic_bytes(ss, S, N, len(qs) if a.workload != "cfg4" else 0)
 
     for _ in range(a.warmup):
         step()
@@ -157,20 +185,25 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": ms_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if a.workload != "cfg4" else "strong",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic: Pareto(1.5)+1 float64 generated on GPU (seed %d + rank)" % a.seed,
-        "config": {"workload": "cfg3: %d streams x %d values per GPU, eps=%g, ingest + quantiles(.5,.9,.99)"
-                               % (S, L, a.eps),
+        "data": "synthetic: %s float64 generated on GPU (seed %d + rank)" % (
+            "Pareto(1.5)+1" if dist_name == "pareto" else "lognormal(0,1)", a.seed),
+        "config": {"workload": ("%s: %d streams x %d values per GPU, eps=%g, %s, ingest + quantiles(.5,.9,.99)"
+                                % (a.workload, S, L, a.eps, dist_name)) if a.workload != "cfg4" else
+                               ("cfg4: %d streams x %d values, row-sharded %d values per stream per GPU, "
+                                "eps=%g, ingest + all-gather + rank-ordered merge + quantiles"
+                                % (S, L * world, L, a.eps)),
                    "streams_per_gpu": S, "values_per_stream": L, "eps": a.eps,
-                   "parallelism": "stream-sharded x%d (no collective)" % world},
+                   "parallelism": ("stream-sharded x%d (no collective)" % world) if a.workload != "cfg4"
+                   else ("row-sharded x%d, RCCL all-gather + merge" % world)},
         "roofline": {"bound": "hbm", "kernel": "k_ingest", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "bytes_per_launch": bytes_per_launch, "launch_ms": k_ms,
                      "stats_kernel_ms": stats_ms / max(launches, 1)},
     }
-    if rank == 0 and world == 1 and not a.no_cpu:
+    if rank == 0 and world == 1 and not a.no_cpu and a.workload != "cfg4":
         threads = a.cpu_threads or min(16, os.cpu_count() or 1)
         line["cpu_baseline"] = cpu_baseline(x, L, min(a.cpu_sample, S), threads, a.eps, q.cpu().numpy())
     if rank == 0:

@@ -1,0 +1,158 @@
+"""Multi-GPU helpers: one process per GPU, torch.distributed (RCCL over xGMI
+with backend "nccl"; gloo on CPU for tests).
+
+Two ways streams meet several GPUs:
+
+* **stream-sharded** -- every stream lives on exactly one rank
+  (``stream_range``); ranks never talk on the data path (weak scaling).
+* **row-sharded** -- every rank sketched a slice of the rows of the SAME
+  streams; the sketches are combined with the reference's left fold
+  ``sk_0.merge(sk_1) ... .merge(sk_{N-1})`` (gk:111-154).  ``merge_row_shards``
+  all-gathers the per-rank states (sizes first, then padded payloads) and each
+  rank folds, in rank order, the streams of its own range -- the merge work is
+  split N ways and the result is stream-sharded.
+
+The exchange helpers (``pack_state`` / ``unpack_state`` / ``all_gather_varlen``
+/ ``allgather_states`` / ``slice_state``) work on tensors of any device, so the
+same code runs over gloo on CPU tensors.
+"""
+import torch
+import torch.distributed as dist
+
+__all__ = ["stream_range", "balanced_assignment", "pack_state", "unpack_state", "all_gather_varlen",
+           "allgather_states", "slice_state", "concat_states", "fold_states", "merge_row_shards"]
+
+_F64 = ("v", "pv", "min", "max", "sum", "avg")
+_I64 = ("offs", "poffs", "n")
+_I32 = ("g", "d")
+
+
+def stream_range(S, world, rank):
+    """Contiguous, balanced stream range [a, b) of `rank` out of `world`."""
+    q, r = divmod(S, world)
+    a = rank * q + min(rank, r)
+    return a, a + q + (1 if rank < r else 0)
+
+
+def balanced_assignment(lengths, world):
+    """Longest-first greedy assignment of streams to ranks by total length
+    (skewed / Zipf stream lengths).  Returns a list of index tensors."""
+    lengths = torch.as_tensor(lengths, dtype=torch.int64).cpu()
+    order = torch.argsort(lengths, descending=True).tolist()
+    load = [0] * world
+    parts = [[] for _ in range(world)]
+    for s in order:
+        k = min(range(world), key=lambda i: load[i])
+        parts[k].append(s)
+        load[k] += int(lengths[s])
+    return [torch.tensor(sorted(p), dtype=torch.int64) for p in parts]
+
+
+def pack_state(state):
+    """State dict (StreamSet.export_state) -> three flat tensors + lengths."""
+    lens = [int(state[k].numel()) for k in _F64 + _I64 + _I32]
+    f = torch.cat([state[k].reshape(-1).to(torch.float64) for k in _F64])
+    i = torch.cat([state[k].reshape(-1).to(torch.int64) for k in _I64])
+    j = torch.cat([state[k].reshape(-1).to(torch.int32) for k in _I32])
+    return f, i, j, lens
+
+
+def unpack_state(f, i, j, lens, eps):
+    names = _F64 + _I64 + _I32
+    out = {"eps": eps}
+    o = {"f": 0, "i": 0, "j": 0}
+    for name, n in zip(names, lens):
+        src, key = (f, "f") if name in _F64 else ((i, "i") if name in _I64 else (j, "j"))
+        out[name] = src[o[key]:o[key] + n]
+        o[key] += n
+    return out
+
+
+def all_gather_varlen(t, group=None):
+    """all_gather of 1-D tensors whose length differs by rank (sizes first,
+    then payloads padded to the longest)."""
+    world = dist.get_world_size(group)
+    n = torch.tensor([t.numel()], dtype=torch.int64, device=t.device)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    sizes = [int(s.item()) for s in sizes]
+    m = max(sizes) if sizes else 0
+    pad = torch.zeros(m, dtype=t.dtype, device=t.device)
+    pad[:t.numel()] = t
+    bufs = [torch.empty(m, dtype=t.dtype, device=t.device) for _ in range(world)]
+    dist.all_gather(bufs, pad, group=group)
+    return [b[:s] for b, s in zip(bufs, sizes)]
+
+
+def allgather_states(state, group=None):
+    """Every rank's state (list indexed by rank), on this rank's device."""
+    f, i, j, lens = pack_state(state)
+    fs = all_gather_varlen(f, group)
+    is_ = all_gather_varlen(i, group)
+    js = all_gather_varlen(j, group)
+    lt = all_gather_varlen(torch.tensor(lens, dtype=torch.int64, device=f.device), group)
+    return [unpack_state(a, b, c, [int(x) for x in l.tolist()], state["eps"])
+            for a, b, c, l in zip(fs, is_, js, lt)]
+
+
+def slice_state(state, a, b):
+    """The state of streams [a, b) of a CSR state dict."""
+    offs, poffs = state["offs"], state["poffs"]
+    t0, t1 = int(offs[a]), int(offs[b])
+    p0, p1 = int(poffs[a]), int(poffs[b])
+    return {"eps": state["eps"],
+            "offs": offs[a:b + 1] - offs[a], "v": state["v"][t0:t1], "g": state["g"][t0:t1],
+            "d": state["d"][t0:t1], "poffs": poffs[a:b + 1] - poffs[a], "pv": state["pv"][p0:p1],
+            "n": state["n"][a:b], "min": state["min"][a:b], "max": state["max"][a:b],
+            "sum": state["sum"][a:b], "avg": state["avg"][a:b]}
+
+
+def concat_states(states):
+    """Streams of several states, in order, as one state."""
+    out = {"eps": states[0]["eps"]}
+    for k in ("v", "g", "d", "pv", "n", "min", "max", "sum", "avg"):
+        out[k] = torch.cat([s[k] for s in states])
+    for k in ("offs", "poffs"):
+        parts, base = [], 0
+        for s in states:
+            parts.append(s[k][:-1] + base)
+            base += int(s[k][-1])
+        parts.append(torch.tensor([base], dtype=torch.int64, device=states[0][k].device))
+        out[k] = torch.cat(parts)
+    return out
+
+
+def fold_states(states, device=None):
+    """Left fold states[0].merge(states[1])...merge(states[-1]) on the GPU,
+    stream by stream (gk:111-154).  Returns the resulting StreamSet."""
+    from .streamset import StreamSet
+    S = int(states[0]["n"].numel())
+    eps = states[0]["eps"]
+    acc = StreamSet(S, eps, device=device)
+    acc.import_state(states[0])
+    others = []
+    for st in states[1:]:
+        o = StreamSet(S, eps, device=device)
+        o.import_state(st)
+        others.append(o)
+    if others:
+        acc.merge_from(others)
+    return acc
+
+
+def merge_row_shards(ss, group=None):
+    """Row-sharded sketches -> merged sketches of this rank's stream range.
+
+    `ss` is this rank's StreamSet over all S streams (built from its slice of
+    the rows).  Returns (StreamSet over streams [a, b), (a, b)); the fold is in
+    rank order, identical to the reference's sk0.merge(sk1)...merge(skN-1).
+    """
+    if not (dist.is_available() and dist.is_initialized()):
+        states, world, rank = [ss.export_state()], 1, 0
+    else:
+        world = dist.get_world_size(group)
+        rank = dist.get_rank(group)
+        states = allgather_states(ss.export_state(), group)
+    a, b = stream_range(ss.num_streams, world, rank)
+    mine = [slice_state(st, a, b) for st in states]
+    return fold_states(mine, device=ss.device), (a, b)

@@ -1,0 +1,177 @@
+"""Multi-rank paths of gkarray_amd.dist.
+
+CPU (gloo, world_size 2, 127.0.0.1): the state exchange (sizes, padded
+payloads, unpacking), the stream ranges and the rank-ordered fold, with the
+per-stream merges done by the oracle on the gathered states and compared with
+the single-process left fold of all shards (gk:111-154).
+GPU: the same fold on one GPU over 8 virtual row shards (only the transport
+differs from an 8-GPU run).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from gk_oracle import OracleGK
+from gk_oracle_c import OracleSet
+from gkarray_amd import dist as gd
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def shard_data(rank, S, eps, seed=5):
+    """Row shard `rank`: per stream, a rank-dependent number of values."""
+    rng = np.random.default_rng(seed * 1000 + rank)
+    P = int(1.0 / eps) + 1
+    lens = rng.integers(0, 6 * P, S)
+    lens[rank % S] = 0  # some empty sides
+    vals = [rng.lognormal(0, 1, int(L)) for L in lens]
+    offs = np.zeros(S + 1, np.int64)
+    offs[1:] = np.cumsum(lens)
+    return np.concatenate(vals) if S else np.zeros(0), offs
+
+
+def oracle_state(flat, offs, S, eps):
+    o = OracleSet(S, eps)
+    o.ingest(flat, offs)
+    to, v, g, d = o.tables()
+    po, pv = o.pending()
+    st = o.stats()
+    t = torch.from_numpy
+    return {"eps": eps, "offs": t(to), "v": t(v), "g": t(g.astype(np.int32)), "d": t(d.astype(np.int32)),
+            "poffs": t(po), "pv": t(pv), "n": t(st["n"].copy()), "min": t(st["min"].copy()),
+            "max": t(st["max"].copy()), "sum": t(st["sum"].copy()), "avg": t(st["avg"].copy())}
+
+
+def oracle_streams_from_state(state):
+    out = []
+    S = int(state["n"].numel())
+    for s in range(S):
+        o = OracleGK(state["eps"])
+        a, b = int(state["offs"][s]), int(state["offs"][s + 1])
+        o.v = state["v"][a:b].tolist()
+        o.g = [int(x) for x in state["g"][a:b].tolist()]
+        o.d = [int(x) for x in state["d"][a:b].tolist()]
+        pa, pb = int(state["poffs"][s]), int(state["poffs"][s + 1])
+        o.pending = state["pv"][pa:pb].tolist()
+        o.n = int(state["n"][s])
+        o.min, o.max = float(state["min"][s]), float(state["max"][s])
+        o.sum, o.avg = float(state["sum"][s]), float(state["avg"][s])
+        out.append(o)
+    return out
+
+
+def same_state(a, b):
+    for k in ("offs", "poffs", "n", "g", "d"):
+        if not torch.equal(a[k].to(torch.int64), b[k].to(torch.int64)):
+            return False
+    for k in ("v", "pv", "min", "max", "sum", "avg"):
+        if not torch.equal(a[k].view(torch.int64), b[k].view(torch.int64)):
+            return False
+    return True
+
+
+def _worker(rank, world, port, S, eps, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mine = oracle_state(*shard_data(rank, S, eps), S, eps)
+        states = gd.allgather_states(mine)
+        ok_exchange = all(same_state(states[r], oracle_state(*shard_data(r, S, eps), S, eps))
+                          for r in range(world))
+        a, b = gd.stream_range(S, world, rank)
+        parts = [oracle_streams_from_state(gd.slice_state(st, a, b)) for st in states]
+        acc = parts[0]
+        for other in parts[1:]:
+            for x, y in zip(acc, other):
+                x.merge(y)
+        res = [(o.table(), o.n, o.min, o.max) for o in acc]
+        q.put((rank, ok_exchange, (a, b), res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_two_rank_row_shard_fold():
+    S, eps, world = 40, 0.05, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, S, eps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # single-process reference: every shard ingested, then the rank-ordered fold
+    shards = [oracle_streams_from_state(oracle_state(*shard_data(r, S, eps), S, eps)) for r in range(world)]
+    ref = shards[0]
+    for other in shards[1:]:
+        for x, y in zip(ref, other):
+            x.merge(y)
+    covered = []
+    for rank, ok_exchange, (a, b), res in sorted(results):
+        assert ok_exchange, "rank %d received wrong states" % rank
+        assert (a, b) == gd.stream_range(S, world, rank)
+        for s, (tab, n, mn, mx) in zip(range(a, b), res):
+            assert tab == ref[s].table() and n == ref[s].n
+            assert mn == ref[s].min and mx == ref[s].max
+        covered.extend(range(a, b))
+    assert covered == list(range(S))
+
+
+def test_stream_range_and_balance():
+    for S in (0, 1, 7, 100, 1001):
+        for w in (1, 2, 3, 8):
+            rs = [gd.stream_range(S, w, r) for r in range(w)]
+            assert rs[0][0] == 0 and rs[-1][1] == S
+            assert all(rs[i][1] == rs[i + 1][0] for i in range(w - 1))
+            assert max(b - a for a, b in rs) - min(b - a for a, b in rs) <= 1
+    lens = np.random.default_rng(0).zipf(1.5, 1000).clip(1, 10 ** 7)
+    parts = gd.balanced_assignment(lens, 8)
+    assert sorted(torch.cat(parts).tolist()) == list(range(1000))
+    loads = [int(lens[p.numpy()].sum()) for p in parts]
+    assert max(loads) - min(loads) <= int(lens.max())
+
+
+def test_pack_slice_concat_roundtrip():
+    S, eps = 30, 0.1
+    st = oracle_state(*shard_data(0, S, eps), S, eps)
+    f, i, j, lens = gd.pack_state(st)
+    back = gd.unpack_state(f, i, j, lens, eps)
+    assert same_state(st, back)
+    parts = [gd.slice_state(st, a, b) for a, b in ((0, 7), (7, 7), (7, 30))]
+    assert same_state(gd.concat_states(parts), st)
+
+
+@pytest.mark.gpu
+def test_gpu_fold_of_virtual_row_shards(gpu_device):
+    """8 virtual row shards folded on the GPU == the oracle's left fold."""
+    S, eps, K = 300, 0.01, 8
+    states = [oracle_state(*shard_data(r, S, eps, seed=9), S, eps) for r in range(K)]
+    acc = gd.fold_states([{k: (v.to(gpu_device) if torch.is_tensor(v) else v) for k, v in st.items()}
+                          for st in states], device=gpu_device)
+    ref = OracleSet(S, eps)
+    ref.ingest(*shard_data(0, S, eps, seed=9))
+    for r in range(1, K):
+        o = OracleSet(S, eps)
+        o.ingest(*shard_data(r, S, eps, seed=9))
+        ref.merge(o)
+    offs, v, g, d = acc.tables()
+    ro, rv, rg, rd = ref.tables()
+    assert np.array_equal(offs.cpu().numpy(), ro)
+    assert np.array_equal(v.cpu().numpy().view(np.int64), rv.view(np.int64))
+    assert np.array_equal(g.cpu().numpy().astype(np.int64), rg)
+    assert np.array_equal(d.cpu().numpy().astype(np.int64), rd)
+    q = acc.quantiles([0.5, 0.9, 0.99]).cpu().numpy()
+    rq = ref.quantiles([0.5, 0.9, 0.99])
+    assert np.array_equal(q.view(np.int64), rq.view(np.int64))
