@@ -66,6 +66,18 @@ def make_input(S, L, seed, device, dist_name="pareto"):
     return x, offs
 
 
+def pmc_traffic(workload):
+    """HBM bytes per k_ingest launch measured by PMC counters for this workload
+    (profiles/pmc_traffic.json, written from a committed rocprofv3 --pmc run),
+    or None when no profile of this workload is committed."""
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            return json.load(f)[workload]["traffic_bytes"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def algorithmic_bytes(ss, S, N, nq):
     """Bytes one fused k_ingest launch must move on a fresh batch (SURVEY
     8(d)): 8 B per value + offsets + 16 B per table entry read and written +
@@ -199,7 +211,7 @@ def main():
                    "parallelism": ("stream-sharded x%d (no collective)" % world) if a.workload != "cfg4"
                    else ("row-sharded x%d, RCCL all-gather + merge" % world)},
         "roofline": {"bound": "hbm", "kernel": "k_ingest", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(a.workload),
                      "bytes_per_launch": bytes_per_launch, "launch_ms": k_ms,
                      "stats_kernel_ms": stats_ms / max(launches, 1)},
     }
