@@ -390,17 +390,15 @@ __device__ __forceinline__ void emit_value(const FlushBuf& L, double* nv, int32_
 
 // Returns the new table size, or -1 if it would exceed `cap` (nothing is
 // written to the table in that case).  `cur` selects the old buffer; on
-// success the new table is in buffer cur^1 (the same buffer when KMAX > 0).
-// KMAX > 0: the lane's block of at most KMAX entries is cached in registers
-// and the table is updated in place.
+// success the new table is in buffer cur^1.  (The 256 class has its own
+// flush, flush_small, below.)
 // `after_search` runs once every lane has read the old table for the gap
 // search; k_ingest issues the next flush's value loads there, so that the
 // compiler's first vmcnt wait for them lands in the NEXT flush.
-template <int VPL, bool GLOBAL, int KMAX, typename AfterSearch>
+template <int VPL, bool GLOBAL, typename AfterSearch>
 __device__ __forceinline__ int flush_wave(const FlushBuf& L, const int cap, const int cur, const int E,
                                           const double (&xv)[VPL], const int cnt, const int T,
                                           const int lane, AfterSearch&& after_search) {
-  constexpr bool REGS = KMAX > 0;
   // selects, not L.tv[cur]: a runtime index into the pointer pair would put
   // the pair in scratch memory
   const double* __restrict__ tv = cur ? L.tv[1] : L.tv[0];
@@ -465,85 +463,7 @@ __device__ __forceinline__ int flush_wave(const FlushBuf& L, const int cap, cons
   int cin = 0, cout = 0;
   uint32_t incl, total;
   int newE;
-  if constexpr (REGS) {
-    double ev[KMAX];
-    int eg[KMAX], ed[KMAX], em[KMAX], eh[KMAX], eG[KMAX], ek[KMAX];
-    bool ekeep[KMAX];
-#pragma unroll
-    for (int e = 0; e < KMAX; ++e) {
-      const int j = j0 + e;
-      const bool v = e < K && j < E;
-      ev[e] = v ? tv[j] : 0.0;
-      eg[e] = v ? tg[j] : 0;
-      ed[e] = v ? td[j] : 0;
-      em[e] = v ? (int)L.gpk[j] : 0;
-      eh[e] = (v && j + 1 < E) ? tg[j + 1] + td[j + 1] : -1;  // -1: no successor
-      eG[e] = 0;
-      ek[e] = 0;
-      ekeep[e] = false;
-    }
-    for (;;) {
-      if (known && !done) {
-        int c = cin;
-#pragma unroll
-        for (int e = 0; e < KMAX; ++e) {
-          if (e < K && j0 + e < E) {
-            const int Gp = eg[e] + c;
-            const int k = clampi(T - ed[e] - Gp, 0, em[e]);
-            const int G = Gp + k;
-            const bool rem = eh[e] >= 0 && (G + eh[e] <= T);
-            eG[e] = G;
-            ek[e] = k;
-            ekeep[e] = !rem;
-            c = rem ? G : 0;
-          }
-        }
-        cout = c;
-        done = true;
-      }
-      const int pc = wave_shr1(cout, 0);
-      const int pd = wave_shr1((int)done, 1);
-      if (!known && pd) {
-        known = true;
-        cin = pc;
-      }
-      if (__all(done)) break;
-    }
-    uint32_t sm = 0, so = 0;
-#pragma unroll
-    for (int e = 0; e < KMAX; ++e)
-      if (e < K && j0 + e < E) {
-        sm += (uint32_t)em[e];
-        so += (uint32_t)(em[e] - ek[e] + (ekeep[e] ? 1 : 0));
-      }
-    if (lane == tail_lane) {
-      const int mE = (int)L.gpk[E];
-      sm += (uint32_t)mE;
-      so += (uint32_t)((mE + cs - 1) / cs);
-    }
-    incl = wave_incl_scan_u32((sm << 16) | so, lane);
-    total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    newE = (int)(total & 0xffffu);
-    if (newE > cap - 1) return -1;  // one slot stays free for the search padding
-    wsync<GLOBAL>();  // every lane has read the old table and the counts
-    uint32_t base = incl - ((sm << 16) | so);
-#pragma unroll
-    for (int e = 0; e < KMAX; ++e)
-      if (e < K && j0 + e < E) {
-        const int j = j0 + e;
-        L.gpk[j] = base;
-        L.gk[j] = ek[e] | (ekeep[e] ? GK_KEEP_BIT : 0);
-        L.gdel[j] = eG[e] + ed[e] - 1;
-        if (ekeep[e]) {
-          const int pos = (int)(base & 0xffffu) + em[e] - ek[e];
-          nv[pos] = ev[e];
-          ng[pos] = eG[e];
-          nd[pos] = ed[e];
-        }
-        base += ((uint32_t)em[e] << 16) | (uint32_t)(em[e] - ek[e] + (ekeep[e] ? 1 : 0));
-      }
-    if (lane == tail_lane) L.gpk[E] = base;
-  } else {
+  {
     for (;;) {
       if (known && !done) {
         int c = cin;
@@ -702,6 +622,9 @@ __device__ __forceinline__ int flush_wave(const FlushBuf& L, const int cap, cons
 // ===========================================================================
 __device__ __forceinline__ double gk_nan() { return __longlong_as_double(0x7ff8000000000000LL); }
 
+// SV / SI: element strides of the value / g,d arrays (1 for the split
+// arrays of the large classes, 2 / 4 for the GKRec table of the 256 class)
+template <int SV>
 __device__ double percentile_linear_arr(const double* __restrict__ tv, int E, double q) {
   // numpy 2.2.6 _function_base_impl.py: q/100 (l.4257), (n-1)*q (l.107),
   // bounds (l.4748-4750), gamma (l.4632), _lerp (l.4653-4657)
@@ -711,7 +634,7 @@ __device__ double percentile_linear_arr(const double* __restrict__ tv, int E, do
   double a, b;
   if (vi >= (double)(E - 1)) {
     prev = -1.0;
-    a = tv[E - 1];
+    a = tv[(E - 1) * SV];
     b = a;
   } else if (vi < 0.0) {
     prev = 0.0;
@@ -720,8 +643,8 @@ __device__ double percentile_linear_arr(const double* __restrict__ tv, int E, do
   } else {
     prev = floor(vi);
     const int pi = (int)prev;
-    a = tv[pi];
-    b = tv[pi + 1];
+    a = tv[pi * SV];
+    b = tv[(pi + 1) * SV];
   }
   const double gamma = vi - prev;
   const double diff = b - a;
@@ -729,6 +652,7 @@ __device__ double percentile_linear_arr(const double* __restrict__ tv, int E, do
   return a + diff * gamma;
 }
 
+template <int SV, int SI>
 __device__ __attribute__((noinline)) void wave_quantiles(const double* __restrict__ tv, const int32_t* __restrict__ tg,
                                const int32_t* __restrict__ td, int E, int64_t n, double mn, double mx,
                                const GKState& st, const double* __restrict__ qs, int nq, int qmode,
@@ -740,7 +664,7 @@ __device__ __attribute__((noinline)) void wave_quantiles(const double* __restric
   if ((double)n < st.inv_eps) {  // gk:169 / gk:200
     for (int q = lane; q < nq; q += 64) {
       const double qv = qs[q];
-      out[q] = (qv >= 0.0 && qv <= 1.0) ? percentile_linear_arr(tv, E, qv) : gk_nan();
+      out[q] = (qv >= 0.0 && qv <= 1.0) ? percentile_linear_arr<SV>(tv, E, qv) : gk_nan();
     }
     return;
   }
@@ -748,12 +672,12 @@ __device__ __attribute__((noinline)) void wave_quantiles(const double* __restric
   const int j0 = lane * K;
   const int jend = min(j0 + K, E);
   int64_t bsum = 0;
-  for (int j = j0; j < jend; ++j) bsum += tg[j];
+  for (int j = j0; j < jend; ++j) bsum += tg[j * SI];
   const int64_t bex = wave_incl_scan_i64(bsum, lane) - bsum;
   int64_t acc = bex, bmax = INT64_MIN;
   for (int j = j0; j < jend; ++j) {
-    acc += tg[j];
-    const int64_t a = acc + td[j] - 1;
+    acc += tg[j * SI];
+    const int64_t a = acc + td[j * SI] - 1;
     if (a > bmax) bmax = a;
   }
   const int64_t pmax_incl = wave_incl_max_i64(bmax, lane);
@@ -768,8 +692,8 @@ __device__ __attribute__((noinline)) void wave_quantiles(const double* __restric
     int c = 0;
     int64_t run = pmax_ex, a2 = bex;
     for (int j = j0; j < jend; ++j) {
-      a2 += tg[j];
-      const int64_t a = a2 + td[j] - 1;
+      a2 += tg[j * SI];
+      const int64_t a = a2 + td[j * SI] - 1;
       if (a > run) run = a;
       c += (run <= th) ? 1 : 0;
     }
@@ -778,8 +702,8 @@ __device__ __attribute__((noinline)) void wave_quantiles(const double* __restric
       double r;
       if (!valid) r = gk_nan();
       else if (i == 0) r = mn;                          // gk:182-183 / gk:220
-      else if (i < E) r = tv[i - 1];                    // gk:185 / gk:220
-      else r = (qmode == 0) ? mx : tv[E - 1];           // gk:229 / gk:185
+      else if (i < E) r = tv[(i - 1) * SV];                    // gk:185 / gk:220
+      else r = (qmode == 0) ? mx : tv[(E - 1) * SV];           // gk:229 / gk:185
       out[q] = r;
     }
   }
@@ -798,7 +722,6 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
                                                int nq, double* __restrict__ qout, int qmode) {
   constexpr int LCAP = CAP > 0 ? CAP : 1;
   constexpr int LVPL = CAP > 0 ? VPL : 1;
-  constexpr int KMAX = CAP == 256 ? 4 : 0;  // registers cache a lane's block of entries
   __shared__ FlushLDS<LCAP, LVPL> Ls;
   FlushBuf B;
   if constexpr (CAP > 0) {
@@ -884,7 +807,7 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
         }
       };
       n += need;
-      const int nE = flush_wave<VPL, CAP == 0, KMAX>(B, cap, cur, E, xv, cnt, gk_threshold(st, n), lane, prefetch);
+      const int nE = flush_wave<VPL, CAP == 0>(B, cap, cur, E, xv, cnt, gk_threshold(st, n), lane, prefetch);
       if (nE < 0) {
         ok = false;
         break;
@@ -905,7 +828,7 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
         const int cnt = p + (int)rem;
         if (!flushed) gk_load_flush_values<VPL>(xv, pb, p, x ? x + xo + used : pb, cnt, lane);
         n += rem;
-        const int nE = flush_wave<VPL, CAP == 0, KMAX>(B, cap, cur, E, xv, cnt, gk_threshold(st, n), lane, [] {});
+        const int nE = flush_wave<VPL, CAP == 0>(B, cap, cur, E, xv, cnt, gk_threshold(st, n), lane, [] {});
         if (nE < 0) {
           ok = false;
         } else {
@@ -939,7 +862,7 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
       const double* fv = cur ? B.tv[1] : B.tv[0];
       const int32_t* fg = cur ? B.tg[1] : B.tg[0];
       const int32_t* fd = cur ? B.td[1] : B.td[0];
-      if (qs) wave_quantiles(fv, fg, fd, E, n, smn, smx, st, qs, nq, qmode, qout + s * (int64_t)nq, lane);
+      if (qs) wave_quantiles<1, 1>(fv, fg, fd, E, n, smn, smx, st, qs, nq, qmode, qout + s * (int64_t)nq, lane);
       for (int j = lane; j < E; j += 64) {
         GKRec rc;
         rc.v = fv[j];
@@ -954,6 +877,472 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
       st.pend[s] = p;
     }
     wsync<CAP == 0>();
+  }
+}
+
+// ===========================================================================
+// k_ingest_small: k_ingest for the 256 class (E <= 255 entries, P <= 128),
+// which holds every stream at eps >= 1/127 until its table outgrows 255
+// entries.  Same algorithm as flush_wave, laid out for the instruction
+// budget of a flush of ~100 values:
+//  * the table is one GKRec array in LDS (16 B per entry): a lane reads its
+//    block of K entries with 128-bit loads and the emit is one 128-bit store;
+//  * K (entries per lane) is a compile-time 2 or 4, picked by E per flush, so
+//    a lane's entries live in registers without per-entry branches (reads
+//    past E stay inside the array and are masked);
+//  * the gap search is unrolled from the table's power-of-two size (a switch
+//    that falls through), every probe an LDS load with an immediate offset;
+//  * divisions by the tail chunk size max(T,1) are multiplications.
+// ===========================================================================
+#define SMALL_CAP 256
+
+template <int VPL>
+struct SmallLDS {
+  GKRec tab[SMALL_CAP + 2];     // v padded with +inf up to pow2_above(E)-2; [j0+K] read as successor
+  uint32_t gpk[SMALL_CAP + 4];  // per gap: count, then (member base << 16) | out base
+  int2 gkd[SMALL_CAP];          // per entry: (k | KEEP, G + d - 1)
+  double mv[64 * VPL];          // pending values grouped by gap, or sort keys
+  uint32_t mp[64 * VPL];        // their payload (insertion index << 16) | gap
+};
+
+__device__ __forceinline__ void small_pad(GKRec* tab, int E, int lane) {
+  const int hi = gk_pow2_above(E) - 1;
+  for (int j = E + lane; j < hi; j += 64) tab[j].v = __longlong_as_double(0x7ff0000000000000LL);
+}
+
+// a / cs for 0 <= a < 256, cs = max(T,1) >= 1: cs == 1 -> a, cs >= 256 -> 0,
+// else the high half of a * ceil(2^32 / cs) (exact: a * cs < 2^16).
+struct CsDiv {
+  int cs;
+  uint32_t magic;
+  int mode;  // 0: cs == 1, 1: magic, 2: cs >= 256
+  __device__ __forceinline__ int div(int a) const {
+    return mode == 0 ? a : (mode == 2 ? 0 : (int)__umulhi((uint32_t)a, magic));
+  }
+};
+
+__device__ __forceinline__ CsDiv make_csdiv(int T) {
+  CsDiv c;
+  c.cs = T > 1 ? T : 1;
+  c.mode = c.cs == 1 ? 0 : (c.cs >= 256 ? 2 : 1);
+  c.magic = c.mode == 1 ? 0xFFFFFFFFu / (uint32_t)c.cs + 1u : 0u;
+  return c;
+}
+
+// One value x (insertion index i) of gap `gap` at rank `rk` inside its gap:
+// gk:93-99 for gap < E, gk:85-92 for the tail.
+template <int VPL>
+__device__ __forceinline__ void small_emit(SmallLDS<VPL>& L, int E, int totm, const CsDiv& cd, double x,
+                                           int gap, int rk) {
+  const uint32_t pk = L.gpk[gap];
+  if (gap < E) {
+    const int2 kd = L.gkd[gap];
+    const int k = kd.x & ~GK_KEEP_BIT;
+    if (rk >= k) {
+      GKRec r;
+      r.v = x;
+      r.g = 1;
+      r.d = kd.y;
+      L.tab[(int)(pk & 0xffffu) + rk - k] = r;
+    }
+  } else {
+    const int m = totm - (int)(pk >> 16);
+    const int q = cd.div(rk);
+    const int rr = rk - q * cd.cs;
+    if (rr == cd.cs - 1 || rk == m - 1) {
+      GKRec r;
+      r.v = x;
+      r.g = rr + 1;
+      r.d = 0;
+      L.tab[(int)(pk & 0xffffu) + q] = r;
+    }
+  }
+}
+
+// One flush of the 256 class; K entries per lane (E <= 64*K - 1).  Returns
+// the new table size, or -1 if it would exceed SMALL_CAP-1 (the table is then
+// untouched... except for the counts, which the caller discards).
+template <int VPL, int K, typename AfterSearch>
+__device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const double (&xv)[VPL], const int cnt,
+                                           const int T, const int lane, AfterSearch&& after_search) {
+  // ---- gap = #entries <= x (gk:93): search from the padded size down ------
+  int xb[VPL];  // byte offset of the gap's first entry
+#pragma unroll
+  for (int r = 0; r < VPL; ++r) xb[r] = 0;
+  const char* tb = (const char*)L.tab;
+#define GK_PROBE(S_)                                                                          \
+  {                                                                                           \
+    double t_[VPL];                                                                           \
+    _Pragma("unroll") for (int r = 0; r < VPL; ++r) t_[r] =                                   \
+        *(const double*)(tb + xb[r] + ((S_) - 1) * (int)sizeof(GKRec));                       \
+    _Pragma("unroll") for (int r = 0; r < VPL; ++r) xb[r] += (t_[r] <= xv[r]) ? (S_) * (int)sizeof(GKRec) : 0; \
+  }
+  switch (32 - __clz(E)) {  // log2(pow2_above(E))
+    case 8: if constexpr (K > 2) GK_PROBE(128) [[fallthrough]];
+    case 7: GK_PROBE(64) [[fallthrough]];
+    case 6: GK_PROBE(32) [[fallthrough]];
+    case 5: GK_PROBE(16) [[fallthrough]];
+    case 4: GK_PROBE(8) [[fallthrough]];
+    case 3: GK_PROBE(4) [[fallthrough]];
+    case 2: GK_PROBE(2) [[fallthrough]];
+    case 1: GK_PROBE(1) [[fallthrough]];
+    default: break;
+  }
+#undef GK_PROBE
+  int xg[VPL];
+#pragma unroll
+  for (int r = 0; r < VPL; ++r) xg[r] = min(xb[r] / (int)sizeof(GKRec), E);  // +inf steps into the padding
+  after_search();
+
+  // ---- gap counts and each value's slot in its gap ------------------------
+  const int j0 = lane * K;
+  if constexpr (K == 2) *(uint2*)&L.gpk[j0] = make_uint2(0u, 0u);
+  else *(uint4*)&L.gpk[j0] = make_uint4(0u, 0u, 0u, 0u);
+  wsync<false>();
+  uint32_t xs[VPL];
+#pragma unroll
+  for (int r = 0; r < VPL; ++r) xs[r] = (lane + 64 * r < cnt) ? atomicAdd(&L.gpk[xg[r]], 1u) : 0u;
+  wsync<false>();
+  uint32_t mloc = 0;
+#pragma unroll
+  for (int r = 0; r < VPL; ++r) mloc = max(mloc, xs[r] + 1u);
+  const bool use_sort = wave_max_u32(mloc) > GK_RANK_LOOP_MAX;
+
+  // ---- the lane's K entries (+ successor) into registers ------------------
+  double ev[K];
+  int eg[K + 1], ed[K + 1], em[K];
+#pragma unroll
+  for (int e = 0; e <= K; ++e) {
+    const GKRec r = L.tab[j0 + e];
+    const bool v = j0 + e < E;  // past E: stale LDS, masked
+    if (e < K) ev[e] = r.v;
+    eg[e] = v ? r.g : 0;
+    ed[e] = v ? r.d : 0;
+  }
+  {
+    uint32_t mm[K];
+    if constexpr (K == 2) {
+      const uint2 v = *(const uint2*)&L.gpk[j0];
+      mm[0] = v.x; mm[1] = v.y;
+    } else {
+      const uint4 v = *(const uint4*)&L.gpk[j0];
+      mm[0] = v.x; mm[1] = v.y; mm[2] = v.z; mm[3] = v.w;
+    }
+#pragma unroll
+    for (int e = 0; e < K; ++e) em[e] = (j0 + e < E) ? (int)mm[e] : 0;
+  }
+  int eh[K];  // g + d of the successor, -1 if none
+#pragma unroll
+  for (int e = 0; e < K; ++e) eh[e] = (j0 + e + 1 < E) ? eg[e + 1] + ed[e + 1] : -1;
+
+  // ---- carry walk (closed form of gk:93-106), as in flush_wave ------------
+  // lane l+1's carry-in is known at once if lane l's last entry is kept with
+  // carry 0 (then for any carry)
+  const bool has = j0 < E;
+  bool known;
+  {
+    const int g = eg[K - 1], d = ed[K - 1];
+    const int G0 = g + clampi(T - d - g, 0, em[K - 1]);
+    const bool keep0 = !(eh[K - 1] >= 0 && G0 + eh[K - 1] <= T);
+    known = (wave_shr1((int)keep0, 1) != 0) || !has;
+  }
+  bool done = !has;
+  int cin = 0, cout = 0;
+  int eG[K], ek[K];
+  bool ekeep[K];
+#pragma unroll
+  for (int e = 0; e < K; ++e) {
+    eG[e] = 0;
+    ek[e] = 0;
+    ekeep[e] = false;
+  }
+  for (;;) {
+    if (known && !done) {
+      int c = cin;
+#pragma unroll
+      for (int e = 0; e < K; ++e) {
+        const int Gp = eg[e] + c;
+        const int k = clampi(T - ed[e] - Gp, 0, em[e]);
+        const int G = Gp + k;
+        const bool rem = eh[e] >= 0 && (G + eh[e] <= T);
+        eG[e] = G;
+        ek[e] = k;
+        ekeep[e] = !rem;
+        c = rem ? G : 0;
+      }
+      cout = c;
+      done = true;
+    }
+    const int pc = wave_shr1(cout, 0);
+    const int pd = wave_shr1((int)done, 1);
+    if (!known && pd) {
+      known = true;
+      cin = pc;
+    }
+    if (__all(done)) break;
+  }
+  const CsDiv cd = make_csdiv(T);
+  uint32_t sm = 0, so = 0;
+#pragma unroll
+  for (int e = 0; e < K; ++e) {
+    const bool v = j0 + e < E;
+    sm += (uint32_t)em[e];  // 0 past E
+    so += v ? (uint32_t)(em[e] - ek[e] + (ekeep[e] ? 1 : 0)) : 0u;
+  }
+  const int tail_lane = E == 0 ? 0 : (E - 1) / K;
+  if (lane == tail_lane) {
+    const int mE = (int)L.gpk[E];
+    sm += (uint32_t)mE;
+    so += (uint32_t)(cd.cs > 128 ? (mE > 0 ? 1 : 0) : cd.div(mE + cd.cs - 1));
+  }
+  const uint32_t incl = wave_incl_scan_u32((sm << 16) | so, lane);
+  const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+  const int newE = (int)(total & 0xffffu);
+  if (newE > SMALL_CAP - 1) return -1;  // one slot stays free for the search padding
+  wsync<false>();                        // every lane has read the table and the counts
+
+  // ---- per-gap results, kept entries (in place: all entries are in registers)
+  {
+    uint32_t base = incl - ((sm << 16) | so);
+    uint32_t bk[K];
+    int2 kd[K];
+#pragma unroll
+    for (int e = 0; e < K; ++e) {
+      bk[e] = base;
+      kd[e] = make_int2(ek[e] | (ekeep[e] ? GK_KEEP_BIT : 0), eG[e] + ed[e] - 1);
+      if (j0 + e < E && ekeep[e]) {
+        GKRec r;
+        r.v = ev[e];
+        r.g = eG[e];
+        r.d = ed[e];
+        L.tab[(int)(base & 0xffffu) + em[e] - ek[e]] = r;
+      }
+      base += (j0 + e < E) ? (((uint32_t)em[e] << 16) | (uint32_t)(em[e] - ek[e] + (ekeep[e] ? 1 : 0))) : 0u;
+    }
+    if constexpr (K == 2) {
+      *(uint2*)&L.gpk[j0] = make_uint2(bk[0], bk[1]);
+      *(int4*)&L.gkd[j0] = make_int4(kd[0].x, kd[0].y, kd[1].x, kd[1].y);
+    } else {
+      *(uint4*)&L.gpk[j0] = make_uint4(bk[0], bk[1], bk[2], bk[3]);
+      *(int4*)&L.gkd[j0] = make_int4(kd[0].x, kd[0].y, kd[1].x, kd[1].y);
+      *(int4*)&L.gkd[j0 + 2] = make_int4(kd[2].x, kd[2].y, kd[3].x, kd[3].y);
+    }
+    // a later store: wins over the block store of the lane owning index E
+    if (lane == tail_lane) L.gpk[E] = base;
+  }
+  const int totm = (int)(total >> 16);
+  wsync<false>();
+
+  // ---- stable order inside each gap (gk:72), then emit --------------------
+  if (!use_sort) {
+#pragma unroll
+    for (int r = 0; r < VPL; ++r) {
+      const int i = lane + 64 * r;
+      if (i < cnt) {
+        const int pos = (int)(L.gpk[xg[r]] >> 16) + (int)xs[r];
+        L.mv[pos] = xv[r];
+        L.mp[pos] = (uint32_t)i;
+      }
+    }
+    wsync<false>();
+#pragma unroll
+    for (int r = 0; r < VPL; ++r) {
+      const int i = lane + 64 * r;
+      if (i < cnt) {
+        const int gap = xg[r];
+        const int gb = (int)(L.gpk[gap] >> 16);
+        const int ge = gap < E ? (int)(L.gpk[gap + 1] >> 16) : totm;
+        const double x = xv[r];
+        int rk = 0;
+        int t = gb;
+        for (; t + 1 < ge; t += 2) {
+          const double y0 = L.mv[t], y1 = L.mv[t + 1];
+          const int i0 = (int)L.mp[t], i1 = (int)L.mp[t + 1];
+          rk += (int)((y0 < x) | ((y0 == x) & (i0 < i)));
+          rk += (int)((y1 < x) | ((y1 == x) & (i1 < i)));
+        }
+        if (t < ge) {
+          const double y0 = L.mv[t];
+          rk += (int)((y0 < x) | ((y0 == x) & ((int)L.mp[t] < i)));
+        }
+        small_emit(L, E, totm, cd, x, gap, rk);
+      }
+    }
+  } else {
+    constexpr int N = 64 * VPL;
+#pragma unroll
+    for (int r = 0; r < VPL; ++r) {
+      const int i = lane + 64 * r;
+      L.mv[i] = (i < cnt) ? xv[r] : __longlong_as_double(0x7ff0000000000000LL);
+      L.mp[i] = (i < cnt) ? (((uint32_t)i << 16) | (uint32_t)xg[r]) : GK_PAD_PAYLOAD;
+    }
+    wsync<false>();
+    for (int k = 2; k <= N; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int pp = lane; pp < N / 2; pp += 64) {
+          const int i = ((pp & ~(j - 1)) << 1) | (pp & (j - 1));
+          const int l = i + j;
+          const double a = L.mv[i], b = L.mv[l];
+          const uint32_t pa = L.mp[i], pb = L.mp[l];
+          const bool a_gt = (a > b) || (a == b && (pa >> 16) > (pb >> 16));
+          const bool asc = (i & k) == 0;
+          if (a_gt == asc) {
+            L.mv[i] = b;
+            L.mv[l] = a;
+            L.mp[i] = pb;
+            L.mp[l] = pa;
+          }
+        }
+        wsync<false>();
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < VPL; ++r) {
+      const int q = lane + 64 * r;
+      if (q < cnt) {
+        const double x = L.mv[q];
+        const int gap = (int)(L.mp[q] & 0xffffu);
+        const int rk = q - (int)(L.gpk[gap] >> 16);
+        small_emit(L, E, totm, cd, x, gap, rk);
+      }
+    }
+  }
+  small_pad(L.tab, newE, lane);
+  wsync<false>();
+  return newE;
+}
+
+template <int VPL>
+__global__ __launch_bounds__(64) void k_ingest_small(GKState st, const double* __restrict__ x,
+                                                     const int64_t* __restrict__ offs,
+                                                     const int32_t* __restrict__ list, int64_t count, int force,
+                                                     int32_t* __restrict__ ovf_count, int32_t* __restrict__ ovf_list,
+                                                     const double* __restrict__ qs, int nq,
+                                                     double* __restrict__ qout, int qmode) {
+  __shared__ __attribute__((aligned(16))) SmallLDS<VPL> L;
+  const int lane = threadIdx.x;
+  const int P = st.P;
+  const int64_t G = gridDim.x;
+  GKHdrV hv;
+  if ((int64_t)blockIdx.x < count) gk_hdr_issue(hv, st, offs, list ? (int64_t)list[blockIdx.x] : (int64_t)blockIdx.x);
+  for (int64_t w = blockIdx.x; w < count; w += G) {
+    const int64_t s = list ? (int64_t)list[w] : w;
+    const int32_t scls = __builtin_amdgcn_readfirstlane(hv.cls);
+    const int32_t sslot = __builtin_amdgcn_readfirstlane(hv.slot);
+    int p = __builtin_amdgcn_readfirstlane(hv.pend);
+    int E = __builtin_amdgcn_readfirstlane(hv.E);
+    int64_t n = rfl64(hv.n);
+    const int64_t xo = rfl64(hv.xo);
+    const int64_t xe = rfl64(hv.xe);
+    const double smn = __longlong_as_double(rfl64(__double_as_longlong(hv.mn)));
+    const double smx = __longlong_as_double(rfl64(__double_as_longlong(hv.mx)));
+    if (w + G < count) gk_hdr_issue(hv, st, offs, list ? (int64_t)list[w + G] : w + G);
+    if (!list && scls != 0) continue;  // promoted: handled by its class launch
+    const int64_t Lx = xe - xo;
+    // force 1: flush only if values are pending (size/quantile, gk:45, 166, 197)
+    // force 2: unconditional merge_compress() (merge, gk:122, 126, 137)
+    if (Lx <= 0 && !((force == 1 && p > 0) || (force == 2 && n > 0)) && !qs) continue;
+    GKRec* __restrict__ tab = gk_table_ptr_cs(st, s, scls, sslot);
+    double* __restrict__ pb = st.pbuf + s * (int64_t)st.pmax;
+    {
+      // 16-byte records moved as int4: all loads issued before the first wait
+      const int4* __restrict__ t4 = (const int4*)tab;
+      int4 rc[SMALL_CAP / 64];
+#pragma unroll
+      for (int r = 0; r < SMALL_CAP / 64; ++r)
+        rc[r] = (lane + 64 * r < E) ? t4[lane + 64 * r] : make_int4(0, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < SMALL_CAP / 64; ++r)
+        if (lane + 64 * r < E) ((int4*)L.tab)[lane + 64 * r] = rc[r];
+    }
+    // an imported / merged table without room for the padding: promotion
+    bool ok = E <= SMALL_CAP - 1;
+    if (ok) small_pad(L.tab, E, lane);
+    wsync<false>();
+
+    bool flushed = false;  // at least one flush in this call
+    bool final_done = false;
+    int64_t used = 0;
+    int64_t need = P - (n % P);  // adds until n hits the next multiple of P (gk:60)
+    double xv[VPL];
+#pragma unroll
+    for (int r = 0; r < VPL; ++r) xv[r] = 0.0;
+    while (ok) {
+      const bool autof = used + need <= Lx;
+      int64_t nadd;
+      if (autof) {
+        nadd = need;
+      } else {
+        nadd = Lx - used;  // < need: only a requested flush takes these now
+        if (!((force == 1 && p + nadd > 0) || force == 2)) break;
+      }
+      const int cnt = p + (int)nadd;
+      if (!flushed) gk_load_flush_values<VPL>(xv, pb, p, x ? x + xo + used : pb, cnt, lane);
+      const int64_t nused = used + nadd;
+      // the next flush's values (or the leftover tail), loaded one flush ahead
+      const int navail = autof ? (int)min((int64_t)P, Lx - nused) : 0;
+      double xn[VPL];
+#pragma unroll
+      for (int r = 0; r < VPL; ++r) xn[r] = 0.0;
+      auto prefetch = [&]() {
+        if (navail > 0) {
+          const double* base = x + xo + nused;
+#pragma unroll
+          for (int r = 0; r < VPL; ++r) xn[r] = base[min(lane + 64 * r, navail - 1)];
+        }
+      };
+      n += nadd;
+      const int T = gk_threshold(st, n);
+      const int nE = E <= 127 ? flush_small<VPL, 2>(L, E, xv, cnt, T, lane, prefetch)
+                              : flush_small<VPL, 4>(L, E, xv, cnt, T, lane, prefetch);
+      if (nE < 0) {
+        ok = false;
+        break;
+      }
+      E = nE;
+      used = nused;
+      p = 0;
+      need = P;
+      flushed = true;
+#pragma unroll
+      for (int r = 0; r < VPL; ++r) xv[r] = (lane + 64 * r < navail) ? xn[r] : 0.0;
+      if (!autof) {
+        final_done = true;
+        break;
+      }
+    }
+    if (ok && !final_done) {
+      const int64_t rem = Lx - used;  // < need: stays pending
+      if (flushed) {
+#pragma unroll
+        for (int r = 0; r < VPL; ++r)
+          if (lane + 64 * r < rem) pb[lane + 64 * r] = xv[r];
+      } else {
+        for (int64_t i = lane; i < rem; i += 64) pb[p + i] = x[xo + used + i];
+      }
+      p += (int)rem;
+      n += rem;
+    }
+    if (!ok) {
+      // nothing was written back: the stream keeps its pre-call state and is
+      // re-run by the host after promotion to the next capacity class
+      if (lane == 0) {
+        const int k = atomicAdd(ovf_count, 1);
+        ovf_list[k] = (int32_t)s;
+      }
+      wsync<false>();
+      continue;
+    }
+    if (qs)
+      wave_quantiles<2, 4>(&L.tab[0].v, &L.tab[0].g, &L.tab[0].d, E, n, smn, smx, st, qs, nq, qmode,
+                           qout + s * (int64_t)nq, lane);
+    for (int j = lane; j < E; j += 64) ((int4*)tab)[j] = ((const int4*)L.tab)[j];
+    if (lane == 0) {
+      st.n[s] = n;
+      st.E[s] = E;
+      st.pend[s] = p;
+    }
+    wsync<false>();
   }
 }
 
@@ -1394,6 +1783,22 @@ static hipError_t launch_ingest_vpl(int vpl, const GKState& st, const double* x,
 #undef GK_L
 }
 
+template <int VPL>
+static hipError_t launch_ingest_small(const GKState& st, const double* x, const int64_t* offs, const int32_t* list,
+                                      int64_t count, int force, int32_t* ovf_count, int32_t* ovf_list,
+                                      const GKQuery& q, hipStream_t stream) {
+  if (count <= 0) return hipSuccess;
+  int occ = 0;
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_ingest_small<VPL>, 64, 0);
+  if (occ <= 0) occ = 1;
+  int64_t grid = (int64_t)num_cu() * occ * 4;
+  if (grid > count) grid = count;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL((k_ingest_small<VPL>), dim3((unsigned)grid), dim3(64), 0, stream, st, x, offs, list, count,
+                     force, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode);
+  return hipGetLastError();
+}
+
 size_t gk_ingest_ws_bytes(int cap, int vpl) { return gk_flush_ws_bytes(cap, vpl); }
 
 hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x, const int64_t* offs,
@@ -1401,9 +1806,10 @@ hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x
                             int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list, const GKQuery& q,
                             hipStream_t stream) {
   switch (cap) {
-    case 256:
-      return launch_ingest_vpl<256>(vpl, st, x, offs, list, count, force, cap, nullptr, 0, 0, ovf_count, ovf_list,
-                                    q, stream);
+    case SMALL_CAP:
+      if (vpl == 1) return launch_ingest_small<1>(st, x, offs, list, count, force, ovf_count, ovf_list, q, stream);
+      if (vpl == 2) return launch_ingest_small<2>(st, x, offs, list, count, force, ovf_count, ovf_list, q, stream);
+      return hipErrorInvalidValue;
     case 2048:
       return launch_ingest_vpl<2048>(vpl, st, x, offs, list, count, force, cap, nullptr, 0, 0, ovf_count, ovf_list,
                                      q, stream);
