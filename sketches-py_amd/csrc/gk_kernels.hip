@@ -1036,50 +1036,47 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
   for (int e = 0; e < K; ++e) eh[e] = (j0 + e + 1 < E) ? eg[e + 1] + ed[e + 1] : -1;
 
   // ---- carry walk (closed form of gk:93-106), as in flush_wave ------------
-  // lane l+1's carry-in is known at once if lane l's last entry is kept with
-  // carry 0 (then for any carry)
-  const bool has = j0 < E;
-  bool known;
-  {
-    const int g = eg[K - 1], d = ed[K - 1];
-    const int G0 = g + clampi(T - d - g, 0, em[K - 1]);
-    const bool keep0 = !(eh[K - 1] >= 0 && G0 + eh[K - 1] <= T);
-    known = (wave_shr1((int)keep0, 1) != 0) || !has;
-  }
-  bool done = !has;
-  int cin = 0, cout = 0;
-  int eG[K], ek[K];
-  bool ekeep[K];
+  // Per entry, with carry c: k = clamp(a - c, 0, m) (a = T - d - g),
+  // G = g + c + k, removed iff G <= b (b = T - g' - d' of the successor,
+  // INT_MIN without one); the carry out is G if removed, else 0.  Rounds only
+  // propagate carries (5 VALU per entry); k, G and keep are evaluated once
+  // from the resolved carry-in afterwards.
+  int ea[K], eb[K];
 #pragma unroll
   for (int e = 0; e < K; ++e) {
-    eG[e] = 0;
-    ek[e] = 0;
-    ekeep[e] = false;
+    ea[e] = T - ed[e] - eg[e];
+    eb[e] = eh[e] >= 0 ? T - eh[e] : INT_MIN;
   }
+  // lane l+1's carry-in is known at once if lane l's last entry is kept with
+  // carry 0 (G grows with c: then it is kept for any carry)
+  const bool has = j0 < E;
+  bool known = (wave_shr1((int)!(eg[K - 1] + clampi(ea[K - 1], 0, em[K - 1]) <= eb[K - 1]), 1) != 0) || !has;
+  int cin = 0;
   for (;;) {
-    if (known && !done) {
-      int c = cin;
+    int c = cin;
 #pragma unroll
-      for (int e = 0; e < K; ++e) {
-        const int Gp = eg[e] + c;
-        const int k = clampi(T - ed[e] - Gp, 0, em[e]);
-        const int G = Gp + k;
-        const bool rem = eh[e] >= 0 && (G + eh[e] <= T);
-        eG[e] = G;
-        ek[e] = k;
-        ekeep[e] = !rem;
-        c = rem ? G : 0;
-      }
-      cout = c;
-      done = true;
+    for (int e = 0; e < K; ++e) {
+      const int G = eg[e] + c + clampi(ea[e] - c, 0, em[e]);
+      c = G <= eb[e] ? G : 0;
     }
-    const int pc = wave_shr1(cout, 0);
-    const int pd = wave_shr1((int)done, 1);
-    if (!known && pd) {
-      known = true;
-      cin = pc;
+    if (__all(known)) break;
+    // a lane whose left neighbour is known takes its (final) carry-out
+    const int pc = wave_shr1(c, 0);
+    const int pk = wave_shr1((int)known, 1);
+    cin = known ? cin : pc;
+    known = known || pk != 0;
+  }
+  int eG[K], ek[K];
+  bool ekeep[K];
+  {
+    int c = cin;
+#pragma unroll
+    for (int e = 0; e < K; ++e) {
+      ek[e] = clampi(ea[e] - c, 0, em[e]);
+      eG[e] = eg[e] + c + ek[e];
+      ekeep[e] = !(eG[e] <= eb[e]);
+      c = ekeep[e] ? 0 : eG[e];
     }
-    if (__all(done)) break;
   }
   const CsDiv cd = make_csdiv(T);
   uint32_t sm = 0, so = 0;

@@ -43,11 +43,12 @@ def main(d, n_values, streams):
     write, wnames = per_dispatch(rows(os.path.join(d, "write", "*counter_collection.csv")), "WRITE_SIZE")
 
     def avg_of(agg, names, key):
-        v = [agg[k] for k in agg if key in names[k]]
+        v = [agg[k] for k in agg if any(x in names[k] for x in key.split("|"))]
         return sum(v) / len(v) if v else None
 
-    f_ing = avg_of(fetch, fnames, "k_ingest<256")
-    w_ing = avg_of(write, wnames, "k_ingest<256")
+    ing = "k_ingest_small|k_ingest<256"  # the class-256 ingest kernel (current | round-1 name)
+    f_ing = avg_of(fetch, fnames, ing)
+    w_ing = avg_of(write, wnames, ing)
     f_st = avg_of(fetch, fnames, "k_stats")
     cal = None
     if f_st:
