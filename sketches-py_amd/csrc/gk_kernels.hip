@@ -39,6 +39,13 @@ __device__ __forceinline__ int gk_threshold(const GKState& st, int64_t n) {
 
 __device__ __forceinline__ int clampi(int x, int lo, int hi) { return x < lo ? lo : (x > hi ? hi : x); }
 
+// clamp(x, 0, m) for m >= 0 in one VALU op (the median of x, 0, m)
+__device__ __forceinline__ int clamp0(int x, int m) {
+  int r;
+  asm("v_med3_i32 %0, %1, 0, %2" : "=v"(r) : "v"(x), "v"(m));
+  return r;
+}
+
 // ---------------------------------------------------------------------------
 // wave helpers (wave64)
 // ---------------------------------------------------------------------------
@@ -896,6 +903,25 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
 // ===========================================================================
 #define SMALL_CAP 256
 
+// Section profiler (profiling builds only, -DGK_PROF; tools/prof_sections.py):
+// lane 0 adds the s_memtime delta since the previous mark to a per-block
+// LDS counter; the block adds its counters to gk_prof_acc when it ends.
+#define GK_PROF_NSEC 12
+#ifdef GK_PROF
+__device__ unsigned long long gk_prof_acc[GK_PROF_NSEC];
+__device__ __forceinline__ uint32_t gk_cycles() { return (uint32_t)__builtin_amdgcn_s_memtime(); }
+#define GK_MARK(L, sec)                                      \
+  do {                                                       \
+    if (threadIdx.x == 0) {                                  \
+      const uint32_t t_ = gk_cycles();                       \
+      (L).prof[sec] += (uint32_t)(t_ - (L).prof_t);         \
+      (L).prof_t = t_;                                       \
+    }                                                        \
+  } while (0)
+#else
+#define GK_MARK(L, sec) do { } while (0)
+#endif
+
 template <int VPL>
 struct SmallLDS {
   GKRec tab[SMALL_CAP + 2];     // v padded with +inf up to pow2_above(E)-2; [j0+K] read as successor
@@ -903,6 +929,10 @@ struct SmallLDS {
   int2 gkd[SMALL_CAP];          // per entry: (k | KEEP, G + d - 1)
   double mv[64 * VPL];          // pending values grouped by gap, or sort keys
   uint32_t mp[64 * VPL];        // their payload (insertion index << 16) | gap
+#ifdef GK_PROF
+  unsigned long long prof[GK_PROF_NSEC];
+  uint32_t prof_t;
+#endif
 };
 
 __device__ __forceinline__ void small_pad(GKRec* tab, int E, int lane) {
@@ -921,11 +951,19 @@ struct CsDiv {
   }
 };
 
+struct CsMagicTable {
+  uint32_t m[256];
+  constexpr CsMagicTable() : m() {
+    for (int c = 2; c < 256; ++c) m[c] = 0xFFFFFFFFu / (uint32_t)c + 1u;
+  }
+};
+__constant__ CsMagicTable gk_cs_magic = CsMagicTable();
+
 __device__ __forceinline__ CsDiv make_csdiv(int T) {
   CsDiv c;
   c.cs = T > 1 ? T : 1;
   c.mode = c.cs == 1 ? 0 : (c.cs >= 256 ? 2 : 1);
-  c.magic = c.mode == 1 ? 0xFFFFFFFFu / (uint32_t)c.cs + 1u : 0u;
+  c.magic = gk_cs_magic.m[c.cs & 255];
   return c;
 }
 
@@ -991,8 +1029,9 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
 #undef GK_PROBE
   int xg[VPL];
 #pragma unroll
-  for (int r = 0; r < VPL; ++r) xg[r] = min(xb[r] / (int)sizeof(GKRec), E);  // +inf steps into the padding
+  for (int r = 0; r < VPL; ++r) xg[r] = min((int)((uint32_t)xb[r] >> 4), E);  // /16; +inf steps into the padding
   after_search();
+  GK_MARK(L, 1);
 
   // ---- gap counts and each value's slot in its gap ------------------------
   const int j0 = lane * K;
@@ -1007,6 +1046,7 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
 #pragma unroll
   for (int r = 0; r < VPL; ++r) mloc = max(mloc, xs[r] + 1u);
   const bool use_sort = wave_max_u32(mloc) > GK_RANK_LOOP_MAX;
+  GK_MARK(L, 2);
 
   // ---- the lane's K entries (+ successor) into registers ------------------
   double ev[K];
@@ -1050,21 +1090,22 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
   // lane l+1's carry-in is known at once if lane l's last entry is kept with
   // carry 0 (G grows with c: then it is kept for any carry)
   const bool has = j0 < E;
-  bool known = (wave_shr1((int)!(eg[K - 1] + clampi(ea[K - 1], 0, em[K - 1]) <= eb[K - 1]), 1) != 0) || !has;
+  const bool known = (wave_shr1((int)!(eg[K - 1] + clamp0(ea[K - 1], em[K - 1]) <= eb[K - 1]), 1) != 0) || !has;
+  // Lane l's carry-in is final once every lane of the run of unknown lanes
+  // ending at l has been re-evaluated: the number of extra rounds is the
+  // longest run of unknown lanes (scalar bit arithmetic on the lane mask).
+  int rounds = 0;
+  for (uint64_t u = ~__builtin_amdgcn_ballot_w64(known); u; u &= u << 1) ++rounds;
   int cin = 0;
-  for (;;) {
+  for (int r = 0; r < rounds; ++r) {
     int c = cin;
 #pragma unroll
     for (int e = 0; e < K; ++e) {
-      const int G = eg[e] + c + clampi(ea[e] - c, 0, em[e]);
+      const int G = eg[e] + c + clamp0(ea[e] - c, em[e]);
       c = G <= eb[e] ? G : 0;
     }
-    if (__all(known)) break;
-    // a lane whose left neighbour is known takes its (final) carry-out
     const int pc = wave_shr1(c, 0);
-    const int pk = wave_shr1((int)known, 1);
-    cin = known ? cin : pc;
-    known = known || pk != 0;
+    cin = known ? 0 : pc;
   }
   int eG[K], ek[K];
   bool ekeep[K];
@@ -1072,7 +1113,7 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
     int c = cin;
 #pragma unroll
     for (int e = 0; e < K; ++e) {
-      ek[e] = clampi(ea[e] - c, 0, em[e]);
+      ek[e] = clamp0(ea[e] - c, em[e]);
       eG[e] = eg[e] + c + ek[e];
       ekeep[e] = !(eG[e] <= eb[e]);
       c = ekeep[e] ? 0 : eG[e];
@@ -1097,6 +1138,7 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
   const int newE = (int)(total & 0xffffu);
   if (newE > SMALL_CAP - 1) return -1;  // one slot stays free for the search padding
   wsync<false>();                        // every lane has read the table and the counts
+  GK_MARK(L, 3);
 
   // ---- per-gap results, kept entries (in place: all entries are in registers)
   {
@@ -1129,6 +1171,7 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
   }
   const int totm = (int)(total >> 16);
   wsync<false>();
+  GK_MARK(L, 4);
 
   // ---- stable order inside each gap (gk:72), then emit --------------------
   if (!use_sort) {
@@ -1165,6 +1208,7 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
         small_emit(L, E, totm, cd, x, gap, rk);
       }
     }
+    GK_MARK(L, 5);
   } else {
     constexpr int N = 64 * VPL;
 #pragma unroll
@@ -1203,9 +1247,11 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
         small_emit(L, E, totm, cd, x, gap, rk);
       }
     }
+    GK_MARK(L, 6);
   }
   small_pad(L.tab, newE, lane);
   wsync<false>();
+  GK_MARK(L, 7);
   return newE;
 }
 
@@ -1220,6 +1266,12 @@ __global__ __launch_bounds__(64) void k_ingest_small(GKState st, const double* _
   const int lane = threadIdx.x;
   const int P = st.P;
   const int64_t G = gridDim.x;
+#ifdef GK_PROF
+  if (lane == 0) {
+    for (int i = 0; i < GK_PROF_NSEC; ++i) L.prof[i] = 0;
+    L.prof_t = gk_cycles();
+  }
+#endif
   GKHdrV hv;
   if ((int64_t)blockIdx.x < count) gk_hdr_issue(hv, st, offs, list ? (int64_t)list[blockIdx.x] : (int64_t)blockIdx.x);
   for (int64_t w = blockIdx.x; w < count; w += G) {
@@ -1256,6 +1308,7 @@ __global__ __launch_bounds__(64) void k_ingest_small(GKState st, const double* _
     bool ok = E <= SMALL_CAP - 1;
     if (ok) small_pad(L.tab, E, lane);
     wsync<false>();
+    GK_MARK(L, 0);
 
     bool flushed = false;  // at least one flush in this call
     bool final_done = false;
@@ -1290,6 +1343,7 @@ __global__ __launch_bounds__(64) void k_ingest_small(GKState st, const double* _
       };
       n += nadd;
       const int T = gk_threshold(st, n);
+      GK_MARK(L, 8);
       const int nE = E <= 127 ? flush_small<VPL, 2>(L, E, xv, cnt, T, lane, prefetch)
                               : flush_small<VPL, 4>(L, E, xv, cnt, T, lane, prefetch);
       if (nE < 0) {
@@ -1340,7 +1394,12 @@ __global__ __launch_bounds__(64) void k_ingest_small(GKState st, const double* _
       st.pend[s] = p;
     }
     wsync<false>();
+    GK_MARK(L, 9);
   }
+#ifdef GK_PROF
+  if (lane == 0)
+    for (int i = 0; i < GK_PROF_NSEC; ++i) atomicAdd(&gk_prof_acc[i], L.prof[i]);
+#endif
 }
 
 // ===========================================================================
@@ -1908,3 +1967,14 @@ hipError_t gk_launch_promote(const GKState& st, const int32_t* list, int64_t cou
                      ncls);
   return hipGetLastError();
 }
+
+#ifdef GK_PROF
+// profiling builds only (not part of include/gk_capi.h)
+extern "C" int gk_prof_read(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(gk_prof_acc), sizeof(unsigned long long) * GK_PROF_NSEC) == hipSuccess ? 0 : -4;
+}
+extern "C" int gk_prof_reset() {
+  unsigned long long z[GK_PROF_NSEC] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(gk_prof_acc), z, sizeof(z)) == hipSuccess ? 0 : -4;
+}
+#endif

@@ -1,0 +1,57 @@
+"""Where k_ingest_small spends its time, by section (profiling build only).
+
+Run on a GPU box after `make -C sketches-py_amd/csrc prof`:
+    python3 tools/prof_sections.py [--workload cfg3|cfg2] [--streams S]
+Loads libgkarray_hip_prof.so (GK_LIB_PATH), runs one bench step (reset +
+fused ingest+quantiles) untimed, then one profiled step, and prints the
+s_memtime cycles accumulated per section over all waves (lane 0 marks, so the
+numbers are per-wave latencies summed; the shares are what matters).
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "sketches-py_amd", "gkarray_amd", "libgkarray_hip_prof.so")
+os.environ.setdefault("GK_LIB_PATH", LIB)
+sys.path.insert(0, os.path.join(ROOT, "sketches-py_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+SECTIONS = ["stream setup (header, table load)", "gap search", "counts (zero, atomics, max gap)",
+            "entries + carry + scan", "keeps + per-gap info", "rank loop + emit", "bitonic sort + emit",
+            "pad + end of flush", "between flushes (values, T)", "leftover, quantiles, write-back", "-", "-"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="cfg3", choices=["cfg3", "cfg2"])
+    ap.add_argument("--streams", type=int, default=0)
+    a = ap.parse_args()
+    from bench import make_input
+    from gkarray_amd import StreamSet
+    S, L, dist_name = {"cfg3": (1_000_000, 1000, "pareto"), "cfg2": (100_000, 10_000, "lognormal")}[a.workload]
+    S = a.streams or S
+    dev = torch.device("cuda", 0)
+    x, offs = make_input(S, L, 3, dev, dist_name)
+    ss = StreamSet(S, 0.01, device=dev)
+    lib = ctypes.CDLL(os.environ["GK_LIB_PATH"])
+    acc = (ctypes.c_ulonglong * 12)()
+    for it in range(2):
+        ss.reset()
+        torch.cuda.synchronize()
+        assert lib.gk_prof_reset() == 0
+        ss.ingest(x, offs, quantiles=[0.5, 0.9, 0.99])
+        torch.cuda.synchronize()
+    assert lib.gk_prof_read(acc) == 0
+    tot = sum(acc)
+    print("workload %s: %d streams x %d values, total %.3e cycles (sum over waves)" % (a.workload, S, L, tot))
+    for i, name in enumerate(SECTIONS):
+        if acc[i]:
+            print("  %2d %-36s %6.1f%%  %.3e" % (i, name, 100.0 * acc[i] / tot, acc[i]))
+
+
+if __name__ == "__main__":
+    main()
