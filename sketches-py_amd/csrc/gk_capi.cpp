@@ -38,7 +38,7 @@ int fail(int code, const char* fmt, ...) {
     if (e_ != hipSuccess) return fail(GK_E_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
   } while (0)
 
-constexpr int kCapSmall = 256;   // LDS class, ~13 KB per wave
+constexpr int kCapSmall = GK_SMALL_CAP;  // LDS class (gk_launch.h)
 constexpr int kCapLarge = 2048;  // LDS class, ~92 KB per wave
 constexpr int kCapHuge = 32768;  // global-workspace class
 constexpr int kMaxLdsCap = 2048;

@@ -901,7 +901,10 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
 //    that falls through), every probe an LDS load with an immediate offset;
 //  * divisions by the tail chunk size max(T,1) are multiplications.
 // ===========================================================================
-#define SMALL_CAP 256
+#define SMALL_CAP GK_SMALL_CAP
+#ifndef GK_SMALL_WAVES
+#define GK_SMALL_WAVES 1  // min waves per SIMD asked of the register allocator
+#endif
 
 // Section profiler (profiling builds only, -DGK_PROF; tools/prof_sections.py):
 // lane 0 adds the s_memtime delta since the previous mark to a per-block
@@ -929,6 +932,9 @@ struct SmallLDS {
   int2 gkd[SMALL_CAP];          // per entry: (k | KEEP, G + d - 1)
   double mv[64 * VPL];          // pending values grouped by gap, or sort keys
   uint32_t mp[64 * VPL];        // their payload (insertion index << 16) | gap
+#ifdef GK_LDS_PAD
+  unsigned char pad[GK_LDS_PAD];  // occupancy experiments only
+#endif
 #ifdef GK_PROF
   unsigned long long prof[GK_PROF_NSEC];
   uint32_t prof_t;
@@ -1256,7 +1262,7 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
 }
 
 template <int VPL>
-__global__ __launch_bounds__(64) void k_ingest_small(GKState st, const double* __restrict__ x,
+__global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st, const double* __restrict__ x,
                                                      const int64_t* __restrict__ offs,
                                                      const int32_t* __restrict__ list, int64_t count, int force,
                                                      int32_t* __restrict__ ovf_count, int32_t* __restrict__ ovf_list,
@@ -1344,8 +1350,12 @@ __global__ __launch_bounds__(64) void k_ingest_small(GKState st, const double* _
       n += nadd;
       const int T = gk_threshold(st, n);
       GK_MARK(L, 8);
-      const int nE = E <= 127 ? flush_small<VPL, 2>(L, E, xv, cnt, T, lane, prefetch)
-                              : flush_small<VPL, 4>(L, E, xv, cnt, T, lane, prefetch);
+      int nE;
+      if constexpr (SMALL_CAP > 128)
+        nE = E <= 127 ? flush_small<VPL, 2>(L, E, xv, cnt, T, lane, prefetch)
+                      : flush_small<VPL, 4>(L, E, xv, cnt, T, lane, prefetch);
+      else
+        nE = flush_small<VPL, 2>(L, E, xv, cnt, T, lane, prefetch);
       if (nE < 0) {
         ok = false;
         break;

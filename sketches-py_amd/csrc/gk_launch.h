@@ -7,6 +7,11 @@
 
 #include "gk_state.h"
 
+// Capacity of the fast LDS class (every stream starts there when P <= 128).
+#ifndef GK_SMALL_CAP
+#define GK_SMALL_CAP 256
+#endif
+
 // optional query fused into an ingest/flush launch (gk:187-232 after the flush)
 struct GKQuery {
   const double* qs = nullptr;  // device, nq values (NULL: no query)
