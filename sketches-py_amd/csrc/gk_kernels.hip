@@ -631,8 +631,8 @@ __device__ __forceinline__ double gk_nan() { return __longlong_as_double(0x7ff80
 
 // SV / SI: element strides of the value / g,d arrays (1 for the split
 // arrays of the large classes, 2 / 4 for the GKRec table of the 256 class)
-template <int SV>
-__device__ double percentile_linear_arr(const double* __restrict__ tv, int E, double q) {
+template <typename At>
+__device__ __forceinline__ double percentile_linear_at(int E, double q, At at) {
   // numpy 2.2.6 _function_base_impl.py: q/100 (l.4257), (n-1)*q (l.107),
   // bounds (l.4748-4750), gamma (l.4632), _lerp (l.4653-4657)
   const double qq = (q * 100.0) / 100.0;
@@ -641,22 +641,27 @@ __device__ double percentile_linear_arr(const double* __restrict__ tv, int E, do
   double a, b;
   if (vi >= (double)(E - 1)) {
     prev = -1.0;
-    a = tv[(E - 1) * SV];
+    a = at(E - 1);
     b = a;
   } else if (vi < 0.0) {
     prev = 0.0;
-    a = tv[0];
+    a = at(0);
     b = a;
   } else {
     prev = floor(vi);
     const int pi = (int)prev;
-    a = tv[pi * SV];
-    b = tv[(pi + 1) * SV];
+    a = at(pi);
+    b = at(pi + 1);
   }
   const double gamma = vi - prev;
   const double diff = b - a;
   if (gamma >= 0.5) return b - diff * (1.0 - gamma);
   return a + diff * gamma;
+}
+
+template <int SV>
+__device__ double percentile_linear_arr(const double* __restrict__ tv, int E, double q) {
+  return percentile_linear_at(E, q, [&](int i) { return tv[i * SV]; });
 }
 
 template <int SV, int SI>
@@ -888,23 +893,35 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
 }
 
 // ===========================================================================
-// k_ingest_small: k_ingest for the 256 class (E <= 255 entries, P <= 128),
-// which holds every stream at eps >= 1/127 until its table outgrows 255
-// entries.  Same algorithm as flush_wave, laid out for the instruction
-// budget of a flush of ~100 values:
-//  * the table is one GKRec array in LDS (16 B per entry): a lane reads its
-//    block of K entries with 128-bit loads and the emit is one 128-bit store;
-//  * K (entries per lane) is a compile-time 2 or 4, picked by E per flush, so
-//    a lane's entries live in registers without per-entry branches (reads
-//    past E stay inside the array and are masked);
+// k_ingest_small: k_ingest for the small LDS class (E <= SMALL_CAP-1 entries,
+// P <= 128), which holds every stream at eps >= 1/127 until its table
+// outgrows the class.  Same algorithm as flush_wave, laid out for the
+// instruction and LDS budget of a flush of ~100 values:
+//  * the table is structure-of-arrays in LDS: values `tv` (8 B) and (g, d)
+//    pairs `tgd` (8 B).  The value array is bank-padded: logical slot i lives
+//    at i + i/32.  The probes of one binary-search level are the slots
+//    S-1 + 2S*m, which without padding all share i mod 32 for S >= 32 (and
+//    crowd onto 2-8 banks below), i.e. up to 32-way LDS bank conflicts; with
+//    the padding every level's probes fall on distinct banks.  The padded
+//    base of a search only changes by S + S/32, so every probe is still an
+//    LDS load with an immediate offset;
+//  * K (entries per lane) is a compile-time 2 or 4 (4 only when the class
+//    holds more than 127 entries), so a lane's entries live in registers
+//    without per-entry branches (reads past E stay inside the arrays and are
+//    masked);
 //  * the gap search is unrolled from the table's power-of-two size (a switch
-//    that falls through), every probe an LDS load with an immediate offset;
-//  * divisions by the tail chunk size max(T,1) are multiplications.
+//    that falls through);
+//  * divisions by the tail chunk size max(T,1) are multiplications;
+//  * quantiles are answered from registers: a lane's K running maxima of
+//    prefix(g) + d - 1, one ballot + popcount per entry slot and quantile.
 // ===========================================================================
 #define SMALL_CAP GK_SMALL_CAP
 #ifndef GK_SMALL_WAVES
-#define GK_SMALL_WAVES 1  // min waves per SIMD asked of the register allocator
+#define GK_SMALL_WAVES 6  // min waves per SIMD asked of the register allocator
 #endif
+// padded index of logical table slot i in the value array
+__device__ __forceinline__ int pidx(int i) { return i + (i >> 5); }
+#define SMALL_TVN (SMALL_CAP + (SMALL_CAP >> 5) + 4)
 
 // Section profiler (profiling builds only, -DGK_PROF; tools/prof_sections.py):
 // lane 0 adds the s_memtime delta since the previous mark to a per-block
@@ -927,7 +944,8 @@ __device__ __forceinline__ uint32_t gk_cycles() { return (uint32_t)__builtin_amd
 
 template <int VPL>
 struct SmallLDS {
-  GKRec tab[SMALL_CAP + 2];     // v padded with +inf up to pow2_above(E)-2; [j0+K] read as successor
+  double tv[SMALL_TVN];         // entry values at pidx(i); +inf from E up to pow2_above(E)-2
+  int2 tgd[SMALL_CAP + 2];      // entry (g, d) at i; [j0+K] read as successor
   uint32_t gpk[SMALL_CAP + 4];  // per gap: count, then (member base << 16) | out base
   int2 gkd[SMALL_CAP];          // per entry: (k | KEEP, G + d - 1)
   double mv[64 * VPL];          // pending values grouped by gap, or sort keys
@@ -941,9 +959,9 @@ struct SmallLDS {
 #endif
 };
 
-__device__ __forceinline__ void small_pad(GKRec* tab, int E, int lane) {
+__device__ __forceinline__ void small_pad(double* tv, int E, int lane) {
   const int hi = gk_pow2_above(E) - 1;
-  for (int j = E + lane; j < hi; j += 64) tab[j].v = __longlong_as_double(0x7ff0000000000000LL);
+  for (int j = E + lane; j < hi; j += 64) tv[pidx(j)] = __longlong_as_double(0x7ff0000000000000LL);
 }
 
 // a / cs for 0 <= a < 256, cs = max(T,1) >= 1: cs == 1 -> a, cs >= 256 -> 0,
@@ -973,6 +991,12 @@ __device__ __forceinline__ CsDiv make_csdiv(int T) {
   return c;
 }
 
+template <int VPL>
+__device__ __forceinline__ void small_put(SmallLDS<VPL>& L, int pos, double v, int g, int d) {
+  L.tv[pidx(pos)] = v;
+  L.tgd[pos] = make_int2(g, d);
+}
+
 // One value x (insertion index i) of gap `gap` at rank `rk` inside its gap:
 // gk:93-99 for gap < E, gk:85-92 for the tail.
 template <int VPL>
@@ -982,44 +1006,34 @@ __device__ __forceinline__ void small_emit(SmallLDS<VPL>& L, int E, int totm, co
   if (gap < E) {
     const int2 kd = L.gkd[gap];
     const int k = kd.x & ~GK_KEEP_BIT;
-    if (rk >= k) {
-      GKRec r;
-      r.v = x;
-      r.g = 1;
-      r.d = kd.y;
-      L.tab[(int)(pk & 0xffffu) + rk - k] = r;
-    }
+    if (rk >= k) small_put(L, (int)(pk & 0xffffu) + rk - k, x, 1, kd.y);
   } else {
     const int m = totm - (int)(pk >> 16);
     const int q = cd.div(rk);
     const int rr = rk - q * cd.cs;
-    if (rr == cd.cs - 1 || rk == m - 1) {
-      GKRec r;
-      r.v = x;
-      r.g = rr + 1;
-      r.d = 0;
-      L.tab[(int)(pk & 0xffffu) + q] = r;
-    }
+    if (rr == cd.cs - 1 || rk == m - 1) small_put(L, (int)(pk & 0xffffu) + q, x, rr + 1, 0);
   }
 }
 
-// One flush of the 256 class; K entries per lane (E <= 64*K - 1).  Returns
+// One flush of the small class; K entries per lane (E <= 64*K - 1).  Returns
 // the new table size, or -1 if it would exceed SMALL_CAP-1 (the table is then
 // untouched... except for the counts, which the caller discards).
 template <int VPL, int K, typename AfterSearch>
 __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const double (&xv)[VPL], const int cnt,
                                            const int T, const int lane, AfterSearch&& after_search) {
   // ---- gap = #entries <= x (gk:93): search from the padded size down ------
-  int xb[VPL];  // byte offset of the gap's first entry
+  // xb: byte offset of the padded slot of the gap's first entry
+  int xb[VPL];
 #pragma unroll
   for (int r = 0; r < VPL; ++r) xb[r] = 0;
-  const char* tb = (const char*)L.tab;
-#define GK_PROBE(S_)                                                                          \
-  {                                                                                           \
-    double t_[VPL];                                                                           \
-    _Pragma("unroll") for (int r = 0; r < VPL; ++r) t_[r] =                                   \
-        *(const double*)(tb + xb[r] + ((S_) - 1) * (int)sizeof(GKRec));                       \
-    _Pragma("unroll") for (int r = 0; r < VPL; ++r) xb[r] += (t_[r] <= xv[r]) ? (S_) * (int)sizeof(GKRec) : 0; \
+  const char* tb = (const char*)L.tv;
+#define GK_PROBE(S_)                                                                                   \
+  {                                                                                                    \
+    constexpr int off_ = ((S_) - 1 + (((S_) - 1) >> 5)) * (int)sizeof(double);                         \
+    constexpr int step_ = ((S_) + ((S_) >> 5)) * (int)sizeof(double);                                  \
+    double t_[VPL];                                                                                    \
+    _Pragma("unroll") for (int r = 0; r < VPL; ++r) t_[r] = *(const double*)(tb + xb[r] + off_);       \
+    _Pragma("unroll") for (int r = 0; r < VPL; ++r) xb[r] += (t_[r] <= xv[r]) ? step_ : 0;             \
   }
   switch (32 - __clz(E)) {  // log2(pow2_above(E))
     case 8: if constexpr (K > 2) GK_PROBE(128) [[fallthrough]];
@@ -1035,7 +1049,10 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
 #undef GK_PROBE
   int xg[VPL];
 #pragma unroll
-  for (int r = 0; r < VPL; ++r) xg[r] = min((int)((uint32_t)xb[r] >> 4), E);  // /16; +inf steps into the padding
+  for (int r = 0; r < VPL; ++r) {
+    const uint32_t p = (uint32_t)xb[r] >> 3;          // padded slot = b + b/32
+    xg[r] = min((int)(p - p / 33u), E);               // +inf steps into the padding
+  }
   after_search();
   GK_MARK(L, 1);
 
@@ -1057,13 +1074,29 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
   // ---- the lane's K entries (+ successor) into registers ------------------
   double ev[K];
   int eg[K + 1], ed[K + 1], em[K];
+  {
+    int2 gd[K + 1];
+    if constexpr (K == 2) {
+      const int4 a = *(const int4*)&L.tgd[j0];
+      gd[0] = make_int2(a.x, a.y);
+      gd[1] = make_int2(a.z, a.w);
+      gd[2] = L.tgd[j0 + 2];
+    } else {
+      const int4 a = *(const int4*)&L.tgd[j0];
+      const int4 b = *(const int4*)&L.tgd[j0 + 2];
+      gd[0] = make_int2(a.x, a.y);
+      gd[1] = make_int2(a.z, a.w);
+      gd[2] = make_int2(b.x, b.y);
+      gd[3] = make_int2(b.z, b.w);
+      gd[4] = L.tgd[j0 + 4];
+    }
 #pragma unroll
-  for (int e = 0; e <= K; ++e) {
-    const GKRec r = L.tab[j0 + e];
-    const bool v = j0 + e < E;  // past E: stale LDS, masked
-    if (e < K) ev[e] = r.v;
-    eg[e] = v ? r.g : 0;
-    ed[e] = v ? r.d : 0;
+    for (int e = 0; e <= K; ++e) {
+      const bool v = j0 + e < E;  // past E: stale LDS, masked
+      if (e < K) ev[e] = L.tv[pidx(j0 + e)];
+      eg[e] = v ? gd[e].x : 0;
+      ed[e] = v ? gd[e].y : 0;
+    }
   }
   {
     uint32_t mm[K];
@@ -1155,13 +1188,7 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
     for (int e = 0; e < K; ++e) {
       bk[e] = base;
       kd[e] = make_int2(ek[e] | (ekeep[e] ? GK_KEEP_BIT : 0), eG[e] + ed[e] - 1);
-      if (j0 + e < E && ekeep[e]) {
-        GKRec r;
-        r.v = ev[e];
-        r.g = eG[e];
-        r.d = ed[e];
-        L.tab[(int)(base & 0xffffu) + em[e] - ek[e]] = r;
-      }
+      if (j0 + e < E && ekeep[e]) small_put(L, (int)(base & 0xffffu) + em[e] - ek[e], ev[e], eG[e], ed[e]);
       base += (j0 + e < E) ? (((uint32_t)em[e] << 16) | (uint32_t)(em[e] - ek[e] + (ekeep[e] ? 1 : 0))) : 0u;
     }
     if constexpr (K == 2) {
@@ -1255,10 +1282,85 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
     }
     GK_MARK(L, 6);
   }
-  small_pad(L.tab, newE, lane);
+  small_pad(L.tv, newE, lane);
   wsync<false>();
   GK_MARK(L, 7);
   return newE;
+}
+
+// Quantiles of one stream from the small-class table (gk:156-232): the same
+// rule as wave_quantiles, with the lane's K entries in registers.  The
+// running max of prefix(g) + d - 1 is monotone, so the reference's break
+// index for a threshold th is the number of entries whose running max is
+// <= th: one ballot + popcount per entry slot.
+template <int K, int VPL>
+__device__ __attribute__((noinline)) void small_quantiles(SmallLDS<VPL>& L, int E, int64_t n, double mn, double mx,
+                                                          const GKState& st, const double* __restrict__ qs, int nq,
+                                                          int qmode, double* __restrict__ out, int lane) {
+  if (n == 0 || E == 0) {
+    for (int q = lane; q < nq; q += 64) out[q] = gk_nan();
+    return;
+  }
+  if ((double)n < st.inv_eps) {  // gk:169 / gk:200
+    for (int q = lane; q < nq; q += 64) {
+      const double qv = qs[q];
+      out[q] = (qv >= 0.0 && qv <= 1.0) ? percentile_linear_at(E, qv, [&](int i) { return L.tv[pidx(i)]; })
+                                        : gk_nan();
+    }
+    return;
+  }
+  const int j0 = lane * K;
+  int64_t run[K];
+  {
+    int g[K], d[K];
+    int lsum = 0;
+#pragma unroll
+    for (int e = 0; e < K; ++e) {
+      const int2 gd = L.tgd[j0 + e];
+      g[e] = (j0 + e < E) ? gd.x : 0;
+      d[e] = gd.y;
+      lsum += g[e];  // <= n - pending of one lane's K entries
+    }
+    const int64_t bex = wave_incl_scan_i64((int64_t)lsum, lane) - (int64_t)lsum;
+    int64_t acc = bex, m = INT64_MIN;
+#pragma unroll
+    for (int e = 0; e < K; ++e) {
+      acc += g[e];
+      const int64_t a = acc + d[e] - 1;
+      if (j0 + e < E && a > m) m = a;
+      run[e] = m;
+    }
+    const int64_t pm = wave_incl_max_i64(m, lane);
+    int64_t pex = __shfl_up(pm, 1, 64);
+    if (lane == 0) pex = INT64_MIN;
+#pragma unroll
+    for (int e = 0; e < K; ++e) run[e] = (j0 + e < E) ? (run[e] > pex ? run[e] : pex) : INT64_MAX;
+  }
+  const int64_t spread = (int64_t)(st.eps * (double)(n - 1));  // gk:174 / gk:210
+  for (int q0 = 0; q0 < nq; q0 += 64) {
+    int myi = 0;
+    const int qe = min(nq - q0, 64);
+    for (int qq = 0; qq < qe; ++qq) {
+      const double qv = qs[q0 + qq];
+      const bool valid = (qv >= 0.0 && qv <= 1.0);
+      const int64_t rank = valid ? (int64_t)(qv * (double)(n - 1) + 1.0) : 0;  // gk:173
+      const int64_t th = rank + spread;
+      int c = 0;
+#pragma unroll
+      for (int e = 0; e < K; ++e) c += __popcll(__builtin_amdgcn_ballot_w64(run[e] <= th));
+      if (lane == qq) myi = c;
+    }
+    if (lane < qe) {
+      const double qv = qs[q0 + lane];
+      const bool valid = (qv >= 0.0 && qv <= 1.0);
+      double r;
+      if (!valid) r = gk_nan();
+      else if (myi == 0) r = mn;                                  // gk:182-183 / gk:220
+      else if (myi < E) r = L.tv[pidx(myi - 1)];                  // gk:185 / gk:220
+      else r = (qmode == 0) ? mx : L.tv[pidx(E - 1)];             // gk:229 / gk:185
+      out[q0 + lane] = r;
+    }
+  }
 }
 
 template <int VPL>
@@ -1299,7 +1401,9 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
     if (Lx <= 0 && !((force == 1 && p > 0) || (force == 2 && n > 0)) && !qs) continue;
     GKRec* __restrict__ tab = gk_table_ptr_cs(st, s, scls, sslot);
     double* __restrict__ pb = st.pbuf + s * (int64_t)st.pmax;
-    {
+    // an imported / merged table without room for the padding: promotion
+    bool ok = E <= SMALL_CAP - 1;
+    if (ok) {
       // 16-byte records moved as int4: all loads issued before the first wait
       const int4* __restrict__ t4 = (const int4*)tab;
       int4 rc[SMALL_CAP / 64];
@@ -1307,12 +1411,15 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
       for (int r = 0; r < SMALL_CAP / 64; ++r)
         rc[r] = (lane + 64 * r < E) ? t4[lane + 64 * r] : make_int4(0, 0, 0, 0);
 #pragma unroll
-      for (int r = 0; r < SMALL_CAP / 64; ++r)
-        if (lane + 64 * r < E) ((int4*)L.tab)[lane + 64 * r] = rc[r];
+      for (int r = 0; r < SMALL_CAP / 64; ++r) {
+        const int j = lane + 64 * r;
+        if (j < E) {
+          L.tv[pidx(j)] = __hiloint2double(rc[r].y, rc[r].x);
+          L.tgd[j] = make_int2(rc[r].z, rc[r].w);
+        }
+      }
+      small_pad(L.tv, E, lane);
     }
-    // an imported / merged table without room for the padding: promotion
-    bool ok = E <= SMALL_CAP - 1;
-    if (ok) small_pad(L.tab, E, lane);
     wsync<false>();
     GK_MARK(L, 0);
 
@@ -1394,10 +1501,19 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
       wsync<false>();
       continue;
     }
-    if (qs)
-      wave_quantiles<2, 4>(&L.tab[0].v, &L.tab[0].g, &L.tab[0].d, E, n, smn, smx, st, qs, nq, qmode,
-                           qout + s * (int64_t)nq, lane);
-    for (int j = lane; j < E; j += 64) ((int4*)tab)[j] = ((const int4*)L.tab)[j];
+    if (qs) {
+      if constexpr (SMALL_CAP > 128) {
+        if (E <= 127) small_quantiles<2>(L, E, n, smn, smx, st, qs, nq, qmode, qout + s * (int64_t)nq, lane);
+        else small_quantiles<4>(L, E, n, smn, smx, st, qs, nq, qmode, qout + s * (int64_t)nq, lane);
+      } else {
+        small_quantiles<2>(L, E, n, smn, smx, st, qs, nq, qmode, qout + s * (int64_t)nq, lane);
+      }
+    }
+    for (int j = lane; j < E; j += 64) {
+      const double v = L.tv[pidx(j)];
+      const int2 gd = L.tgd[j];
+      ((int4*)tab)[j] = make_int4(__double2loint(v), __double2hiint(v), gd.x, gd.y);
+    }
     if (lane == 0) {
       st.n[s] = n;
       st.E[s] = E;

@@ -9,7 +9,7 @@
 
 // Capacity of the fast LDS class (every stream starts there when P <= 128).
 #ifndef GK_SMALL_CAP
-#define GK_SMALL_CAP 256
+#define GK_SMALL_CAP 128
 #endif
 
 // optional query fused into an ingest/flush launch (gk:187-232 after the flush)
