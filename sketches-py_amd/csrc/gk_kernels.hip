@@ -919,6 +919,10 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
 #ifndef GK_SMALL_WAVES
 #define GK_SMALL_WAVES 6  // min waves per SIMD asked of the register allocator
 #endif
+// largest gap handled by the in-gap rank loop; larger gaps rank by counting
+#ifndef GK_SMALL_RANK_MAX
+#define GK_SMALL_RANK_MAX 16
+#endif
 // padded index of logical table slot i in the value array
 __device__ __forceinline__ int pidx(int i) { return i + (i >> 5); }
 #define SMALL_TVN (SMALL_CAP + (SMALL_CAP >> 5) + 4)
@@ -1068,7 +1072,7 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
   uint32_t mloc = 0;
 #pragma unroll
   for (int r = 0; r < VPL; ++r) mloc = max(mloc, xs[r] + 1u);
-  const bool use_sort = wave_max_u32(mloc) > GK_RANK_LOOP_MAX;
+  const bool use_sort = wave_max_u32(mloc) > GK_SMALL_RANK_MAX;
   GK_MARK(L, 2);
 
   // ---- the lane's K entries (+ successor) into registers ------------------
@@ -1243,41 +1247,57 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
     }
     GK_MARK(L, 5);
   } else {
-    constexpr int N = 64 * VPL;
+    // A large gap (the first flush, where every value is tail, or an
+    // adversarial order): each value's rank among all the flush's values, by
+    // counting in registers -- every value is broadcast from its lane
+    // (v_readlane into SGPRs) and compared with the lane's own values.  No
+    // LDS traffic.  Gap members are contiguous in the stable order (gaps
+    // partition the value range), so the rank inside the gap is the global
+    // rank minus the gap's member base.  Equal values (the stable order's
+    // tie-break on insertion index) are rare: strict counting gives tied
+    // values the same rank, which shows as a rank sum below cnt*(cnt-1)/2,
+    // and only then is the exact comparison run.
+    int q[VPL];
 #pragma unroll
-    for (int r = 0; r < VPL; ++r) {
-      const int i = lane + 64 * r;
-      L.mv[i] = (i < cnt) ? xv[r] : __longlong_as_double(0x7ff0000000000000LL);
-      L.mp[i] = (i < cnt) ? (((uint32_t)i << 16) | (uint32_t)xg[r]) : GK_PAD_PAYLOAD;
+    for (int r = 0; r < VPL; ++r) q[r] = 0;
+#pragma unroll
+    for (int r2 = 0; r2 < VPL; ++r2) {
+      if (64 * r2 >= cnt) break;
+      // slots past cnt compare as +inf (never below a value)
+      const double y2 = (lane + 64 * r2 < cnt) ? xv[r2] : __longlong_as_double(0x7ff0000000000000LL);
+      const int lo2 = __double2loint(y2), hi2 = __double2hiint(y2);
+#pragma unroll
+      for (int jl = 0; jl < 64; ++jl) {
+        const double y = __hiloint2double(__builtin_amdgcn_readlane(hi2, jl), __builtin_amdgcn_readlane(lo2, jl));
+#pragma unroll
+        for (int r = 0; r < VPL; ++r) q[r] += (y < xv[r]) ? 1 : 0;
+      }
     }
-    wsync<false>();
-    for (int k = 2; k <= N; k <<= 1) {
-      for (int j = k >> 1; j > 0; j >>= 1) {
-        for (int pp = lane; pp < N / 2; pp += 64) {
-          const int i = ((pp & ~(j - 1)) << 1) | (pp & (j - 1));
-          const int l = i + j;
-          const double a = L.mv[i], b = L.mv[l];
-          const uint32_t pa = L.mp[i], pb = L.mp[l];
-          const bool a_gt = (a > b) || (a == b && (pa >> 16) > (pb >> 16));
-          const bool asc = (i & k) == 0;
-          if (a_gt == asc) {
-            L.mv[i] = b;
-            L.mv[l] = a;
-            L.mp[i] = pb;
-            L.mp[l] = pa;
-          }
+    uint32_t qsum = 0;
+#pragma unroll
+    for (int r = 0; r < VPL; ++r) qsum += (lane + 64 * r < cnt) ? (uint32_t)q[r] : 0u;
+    qsum = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan_u32(qsum, lane), 63);
+    if (qsum != (uint32_t)(cnt * (cnt - 1) / 2)) {
+      // ties: (y < x) or (y == x and earlier), gk:72's stable sort
+#pragma unroll
+      for (int r = 0; r < VPL; ++r) q[r] = 0;
+#pragma unroll
+      for (int r2 = 0; r2 < VPL; ++r2) {
+        const int nj = min(64, cnt - 64 * r2);
+        const int lo2 = __double2loint(xv[r2]), hi2 = __double2hiint(xv[r2]);
+        for (int jl = 0; jl < nj; ++jl) {
+          const double y = __hiloint2double(__builtin_amdgcn_readlane(hi2, jl), __builtin_amdgcn_readlane(lo2, jl));
+          const int j = jl + 64 * r2;
+#pragma unroll
+          for (int r = 0; r < VPL; ++r) q[r] += ((y < xv[r]) | ((y == xv[r]) & (j < lane + 64 * r))) ? 1 : 0;
         }
-        wsync<false>();
       }
     }
 #pragma unroll
     for (int r = 0; r < VPL; ++r) {
-      const int q = lane + 64 * r;
-      if (q < cnt) {
-        const double x = L.mv[q];
-        const int gap = (int)(L.mp[q] & 0xffffu);
-        const int rk = q - (int)(L.gpk[gap] >> 16);
-        small_emit(L, E, totm, cd, x, gap, rk);
+      if (lane + 64 * r < cnt) {
+        const int gap = xg[r];
+        small_emit(L, E, totm, cd, xv[r], gap, q[r] - (int)(L.gpk[gap] >> 16));
       }
     }
     GK_MARK(L, 6);
