@@ -38,16 +38,19 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="cfg3", choices=["cfg3", "cfg2", "cfg4"],
+    ap.add_argument("--workload", default="cfg3", choices=["cfg3", "cfg2", "cfg4", "cfg5"],
                     help="cfg3 (default, the metric's config): 1M streams x 1k Pareto values per GPU; "
                          "cfg2: 100k x 10k lognormal; cfg4: 10k streams x 1M lognormal values "
-                         "row-sharded over the GPUs, merged by all-gather + rank-ordered fold")
+                         "row-sharded over the GPUs, merged by all-gather + rank-ordered fold; "
+                         "cfg5: 100k streams, lengths clip(zipf(1.5), 1, 1e7) (one forced to 1e7), "
+                         "lognormal, eps=0.001")
     ap.add_argument("--streams", type=int, default=None, help="override: streams per GPU (cfg4: total)")
     ap.add_argument("--values", type=int, default=None, help="override: values per stream (cfg4: total)")
-    ap.add_argument("--eps", type=float, default=0.01)
+    ap.add_argument("--eps", type=float, default=None, help="default 0.01 (cfg5: 0.001)")
     ap.add_argument("--seed", type=int, default=3)
-    ap.add_argument("--cpu-sample", type=int, default=300000,
-                    help="streams of the same workload timed on the host oracle (rank 0, N=1)")
+    ap.add_argument("--cpu-sample", type=int, default=1_000_000,
+                    help="streams of the same workload timed on the host oracle (rank 0, N=1); "
+                         "default: the whole cfg3 batch")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, os.cpu_count())")
     ap.add_argument("--no-cpu", action="store_true")
     return ap.parse_args()
@@ -64,6 +67,19 @@ def make_input(S, L, seed, device, dist_name="pareto"):
         x = torch.randn(S * L, dtype=torch.float64, device=device, generator=g).exp_()
     offs = torch.arange(0, S * L + 1, L, dtype=torch.int64, device=device)
     return x, offs
+
+
+def make_zipf_input(S, seed, device, cap=10_000_000):
+    """cfg5: stream lengths clip(zipf(1.5), 1, cap) with stream 0 forced to cap
+    (numpy default_rng(seed)), lognormal(0,1) values on the GPU."""
+    lens = np.clip(np.random.default_rng(seed).zipf(1.5, S), 1, cap).astype(np.int64)
+    lens[0] = cap
+    offs = np.zeros(S + 1, dtype=np.int64)
+    np.cumsum(lens, out=offs[1:])
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    x = torch.randn(int(offs[-1]), dtype=torch.float64, device=device, generator=g).exp_()
+    return x, torch.from_numpy(offs).to(device)
 
 
 def pmc_traffic(workload):
@@ -91,20 +107,22 @@ def algorithmic_bytes(ss, S, N, nq):
             + 8 * nq * S)
 
 
-def cpu_baseline(x, L, sample, threads, eps, gpu_q):
+def cpu_baseline(x, offs, sample, threads, eps, gpu_q):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     from gk_oracle_c import OracleSet
-    xs = x[: sample * L].cpu().numpy()
-    offs = np.arange(0, sample * L + 1, L, dtype=np.int64)
+    o_all = offs[: sample + 1].cpu().numpy()
+    nv = int(o_all[-1] - o_all[0])
+    xs = x[int(o_all[0]): int(o_all[-1])].cpu().numpy()
+    o_loc = o_all - o_all[0]
     o = OracleSet(sample, eps, threads=threads)
     t0 = time.perf_counter()
-    o.ingest(xs, offs)
+    o.ingest(xs, o_loc)
     q = o.quantiles([0.5, 0.9, 0.99])
     dt = time.perf_counter() - t0
     same = np.array_equal(q.view(np.int64), gpu_q[:sample].view(np.int64))
-    return dict(value=sample * L / dt, unit="values/s", cores=threads, kind="port",
-                sample="%d streams x %d values (the first streams of the GPU workload), "
-                       "ingest + quantiles([.5,.9,.99]) in oracle/gk_oracle.c, %.1f s" % (sample, L, dt),
+    return dict(value=nv / dt, unit="values/s", cores=threads, kind="port",
+                sample="%d streams, %d values (the first streams of the GPU workload), "
+                       "ingest + quantiles([.5,.9,.99]) in oracle/gk_oracle.c, %.1f s" % (sample, nv, dt),
                 parity_on_sample=bool(same))
 
 
@@ -121,10 +139,12 @@ def main():
     from gkarray_amd import StreamSet
 
     defaults = {"cfg3": (1_000_000, 1000, "pareto"), "cfg2": (100_000, 10_000, "lognormal"),
-                "cfg4": (10_000, 1_000_000, "lognormal")}
+                "cfg4": (10_000, 1_000_000, "lognormal"), "cfg5": (100_000, 0, "zipf-lengths lognormal")}
     S, L, dist_name = defaults[a.workload]
     S = a.streams or S
     L = a.values or L
+    if a.eps is None:
+        a.eps = 0.001 if a.workload == "cfg5" else 0.01
     qs = [0.5, 0.9, 0.99]
     if a.workload == "cfg4":
         # rows of every stream split over the ranks: this rank sketches its
@@ -143,8 +163,13 @@ def main():
             merged.close()
             return q
     else:
-        N = S * L
-        x, offs = make_input(S, L, a.seed + rank, dev, dist_name)
+        if a.workload == "cfg5":
+            x, offs = make_zipf_input(S, 5 + rank, dev, cap=a.values or 10_000_000)
+            N = x.numel()
+            L = N / S  # mean length
+        else:
+            N = S * L
+            x, offs = make_input(S, L, a.seed + rank, dev, dist_name)
         ss = StreamSet(S, a.eps, device=dev)
 
         def step():
@@ -202,8 +227,10 @@ def main():
         "dtype": "f64",
         "data": "synthetic: %s float64 generated on GPU (seed %d + rank)" % (
             "Pareto(1.5)+1" if dist_name == "pareto" else "lognormal(0,1)", a.seed),
-        "config": {"workload": ("%s: %d streams x %d values per GPU, eps=%g, %s, ingest + quantiles(.5,.9,.99)"
-                                % (a.workload, S, L, a.eps, dist_name)) if a.workload != "cfg4" else
+        "config": {"workload": ("%s: %d streams x %s values per GPU, eps=%g, %s, ingest + quantiles(.5,.9,.99)"
+                                % (a.workload, S, ("%d" % L) if a.workload != "cfg5" else
+                                   ("clip(zipf(1.5),1,1e7) (%d total)" % N), a.eps, dist_name))
+                               if a.workload != "cfg4" else
                                ("cfg4: %d streams x %d values, row-sharded %d values per stream per GPU, "
                                 "eps=%g, ingest + all-gather + rank-ordered merge + quantiles"
                                 % (S, L * world, L, a.eps)),
@@ -217,7 +244,10 @@ def main():
     }
     if rank == 0 and world == 1 and not a.no_cpu and a.workload != "cfg4":
         threads = a.cpu_threads or min(16, os.cpu_count() or 1)
-        line["cpu_baseline"] = cpu_baseline(x, L, min(a.cpu_sample, S), threads, a.eps, q.cpu().numpy())
+        sample = min(a.cpu_sample, S)
+        if a.workload == "cfg5":  # the long streams dominate: a bounded prefix of streams
+            sample = min(sample, 20000)
+        line["cpu_baseline"] = cpu_baseline(x, offs, sample, threads, a.eps, q.cpu().numpy())
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -950,10 +950,9 @@ template <int VPL>
 struct SmallLDS {
   double tv[SMALL_TVN];         // entry values at pidx(i); +inf from E up to pow2_above(E)-2
   int2 tgd[SMALL_CAP + 2];      // entry (g, d) at i; [j0+K] read as successor
-  uint32_t gpk[SMALL_CAP + 4];  // per gap: count, then (member base << 16) | out base
-  int2 gkd[SMALL_CAP];          // per entry: (k | KEEP, G + d - 1)
-  double mv[64 * VPL];          // pending values grouped by gap, or sort keys
-  uint32_t mp[64 * VPL];        // their payload (insertion index << 16) | gap
+  uint32_t gpk[SMALL_CAP + 4];  // per gap: member count
+  int2 gi[SMALL_CAP + 2];       // per gap: (k << 16 | member base << 8 | out base, G + d - 1)
+  double mv[64 * VPL];          // pending values grouped by gap
 #ifdef GK_LDS_PAD
   unsigned char pad[GK_LDS_PAD];  // occupancy experiments only
 #endif
@@ -1003,19 +1002,24 @@ __device__ __forceinline__ void small_put(SmallLDS<VPL>& L, int pos, double v, i
 
 // One value x (insertion index i) of gap `gap` at rank `rk` inside its gap:
 // gk:93-99 for gap < E, gk:85-92 for the tail.
+// gi[gap].x fields
+__device__ __forceinline__ int gi_ob(int x) { return x & 0xff; }
+__device__ __forceinline__ int gi_mb(int x) { return (x >> 8) & 0xff; }
+__device__ __forceinline__ int gi_k(int x) { return x >> 16; }
+
+// One value x of gap `gap` (its info gi) at rank `rk` inside its gap:
+// gk:93-99 for gap < E, gk:85-92 for the tail.
 template <int VPL>
 __device__ __forceinline__ void small_emit(SmallLDS<VPL>& L, int E, int totm, const CsDiv& cd, double x,
-                                           int gap, int rk) {
-  const uint32_t pk = L.gpk[gap];
+                                           int gap, int2 gi, int rk) {
   if (gap < E) {
-    const int2 kd = L.gkd[gap];
-    const int k = kd.x & ~GK_KEEP_BIT;
-    if (rk >= k) small_put(L, (int)(pk & 0xffffu) + rk - k, x, 1, kd.y);
+    const int k = gi_k(gi.x);
+    if (rk >= k) small_put(L, gi_ob(gi.x) + rk - k, x, 1, gi.y);
   } else {
-    const int m = totm - (int)(pk >> 16);
+    const int m = totm - gi_mb(gi.x);
     const int q = cd.div(rk);
     const int rr = rk - q * cd.cs;
-    if (rr == cd.cs - 1 || rk == m - 1) small_put(L, (int)(pk & 0xffffu) + q, x, rr + 1, 0);
+    if (rr == cd.cs - 1 || rk == m - 1) small_put(L, gi_ob(gi.x) + q, x, rr + 1, 0);
   }
 }
 
@@ -1072,7 +1076,17 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
   uint32_t mloc = 0;
 #pragma unroll
   for (int r = 0; r < VPL; ++r) mloc = max(mloc, xs[r] + 1u);
-  const bool use_sort = wave_max_u32(mloc) > GK_SMALL_RANK_MAX;
+  // +0.0 and -0.0 in one flush: only the exact (insertion-index) tie-break
+  // of the counting path orders them like the reference
+  bool pz = false, nz = false;
+#pragma unroll
+  for (int r = 0; r < VPL; ++r) {
+    const bool z = (lane + 64 * r < cnt) && xv[r] == 0.0;
+    pz |= z && !signbit(xv[r]);
+    nz |= z && signbit(xv[r]);
+  }
+  const bool use_sort = (wave_max_u32(mloc) > GK_SMALL_RANK_MAX) ||
+                        (__builtin_amdgcn_ballot_w64(pz) != 0 && __builtin_amdgcn_ballot_w64(nz) != 0);
   GK_MARK(L, 2);
 
   // ---- the lane's K entries (+ successor) into registers ------------------
@@ -1185,26 +1199,18 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
 
   // ---- per-gap results, kept entries (in place: all entries are in registers)
   {
-    uint32_t base = incl - ((sm << 16) | so);
-    uint32_t bk[K];
-    int2 kd[K];
+    uint32_t base = incl - ((sm << 16) | so);  // (member base << 16) | out base
+    int2 gk[K];
 #pragma unroll
     for (int e = 0; e < K; ++e) {
-      bk[e] = base;
-      kd[e] = make_int2(ek[e] | (ekeep[e] ? GK_KEEP_BIT : 0), eG[e] + ed[e] - 1);
+      gk[e] = make_int2((ek[e] << 16) | (int)((base >> 8) & 0xff00u) | (int)(base & 0xffu), eG[e] + ed[e] - 1);
       if (j0 + e < E && ekeep[e]) small_put(L, (int)(base & 0xffffu) + em[e] - ek[e], ev[e], eG[e], ed[e]);
       base += (j0 + e < E) ? (((uint32_t)em[e] << 16) | (uint32_t)(em[e] - ek[e] + (ekeep[e] ? 1 : 0))) : 0u;
     }
-    if constexpr (K == 2) {
-      *(uint2*)&L.gpk[j0] = make_uint2(bk[0], bk[1]);
-      *(int4*)&L.gkd[j0] = make_int4(kd[0].x, kd[0].y, kd[1].x, kd[1].y);
-    } else {
-      *(uint4*)&L.gpk[j0] = make_uint4(bk[0], bk[1], bk[2], bk[3]);
-      *(int4*)&L.gkd[j0] = make_int4(kd[0].x, kd[0].y, kd[1].x, kd[1].y);
-      *(int4*)&L.gkd[j0 + 2] = make_int4(kd[2].x, kd[2].y, kd[3].x, kd[3].y);
-    }
+    *(int4*)&L.gi[j0] = make_int4(gk[0].x, gk[0].y, gk[1].x, gk[1].y);
+    if constexpr (K == 4) *(int4*)&L.gi[j0 + 2] = make_int4(gk[2].x, gk[2].y, gk[3].x, gk[3].y);
     // a later store: wins over the block store of the lane owning index E
-    if (lane == tail_lane) L.gpk[E] = base;
+    if (lane == tail_lane) L.gi[E] = make_int2((int)((base >> 8) & 0xff00u) | (int)(base & 0xffu), 0);
   }
   const int totm = (int)(total >> 16);
   wsync<false>();
@@ -1212,39 +1218,52 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
 
   // ---- stable order inside each gap (gk:72), then emit --------------------
   if (!use_sort) {
+    // Members of a gap are stored in slot order (the atomic slot xs); a
+    // value's rank in its gap counts the members below it, equal members
+    // broken by slot.  The reference breaks ties by insertion order; equal
+    // doubles are bit-identical except +0.0 / -0.0, and a flush holding both
+    // signs of zero takes the exact path below, so the output is the same.
+    int2 gv[VPL];
+    int gb[VPL], mo[VPL], me[VPL];
+    uint32_t omax = 0;
 #pragma unroll
     for (int r = 0; r < VPL; ++r) {
-      const int i = lane + 64 * r;
-      if (i < cnt) {
-        const int pos = (int)(L.gpk[xg[r]] >> 16) + (int)xs[r];
-        L.mv[pos] = xv[r];
-        L.mp[pos] = (uint32_t)i;
-      }
+      const bool v = lane + 64 * r < cnt;
+      const int gap = xg[r];
+      gv[r] = L.gi[gap];
+      const int ge = gap < E ? gi_mb(L.gi[gap + 1].x) : totm;
+      gb[r] = gi_mb(gv[r].x);
+      mo[r] = v ? ge - gb[r] - 1 : 0;  // other members of the gap
+      me[r] = (int)xs[r];
+      if (v) L.mv[gb[r] + me[r]] = xv[r];
+      omax = max(omax, (uint32_t)mo[r]);
     }
+    omax = wave_max_u32(omax);
     wsync<false>();
+    int rk[VPL];
 #pragma unroll
-    for (int r = 0; r < VPL; ++r) {
-      const int i = lane + 64 * r;
-      if (i < cnt) {
-        const int gap = xg[r];
-        const int gb = (int)(L.gpk[gap] >> 16);
-        const int ge = gap < E ? (int)(L.gpk[gap + 1] >> 16) : totm;
-        const double x = xv[r];
-        int rk = 0;
-        int t = gb;
-        for (; t + 1 < ge; t += 2) {
-          const double y0 = L.mv[t], y1 = L.mv[t + 1];
-          const int i0 = (int)L.mp[t], i1 = (int)L.mp[t + 1];
-          rk += (int)((y0 < x) | ((y0 == x) & (i0 < i)));
-          rk += (int)((y1 < x) | ((y1 == x) & (i1 < i)));
+    for (int r = 0; r < VPL; ++r) rk[r] = 0;
+    for (int u0 = 0; u0 < (int)omax; u0 += 2) {
+      double y[VPL][2];
+#pragma unroll
+      for (int r = 0; r < VPL; ++r)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int u = min(u0 + h, max(mo[r] - 1, 0));
+          y[r][h] = L.mv[min(gb[r] + u + (u >= me[r] ? 1 : 0), 64 * VPL - 1)];
         }
-        if (t < ge) {
-          const double y0 = L.mv[t];
-          rk += (int)((y0 < x) | ((y0 == x) & ((int)L.mp[t] < i)));
+#pragma unroll
+      for (int r = 0; r < VPL; ++r)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int u = u0 + h;
+          const bool below = (y[r][h] < xv[r]) | ((y[r][h] == xv[r]) & (u < me[r]));
+          rk[r] += (u < mo[r] && below) ? 1 : 0;
         }
-        small_emit(L, E, totm, cd, x, gap, rk);
-      }
     }
+#pragma unroll
+    for (int r = 0; r < VPL; ++r)
+      if (lane + 64 * r < cnt) small_emit(L, E, totm, cd, xv[r], xg[r], gv[r], rk[r]);
     GK_MARK(L, 5);
   } else {
     // A large gap (the first flush, where every value is tail, or an
@@ -1296,8 +1315,8 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
 #pragma unroll
     for (int r = 0; r < VPL; ++r) {
       if (lane + 64 * r < cnt) {
-        const int gap = xg[r];
-        small_emit(L, E, totm, cd, xv[r], gap, q[r] - (int)(L.gpk[gap] >> 16));
+        const int2 gv = L.gi[xg[r]];
+        small_emit(L, E, totm, cd, xv[r], xg[r], gv, q[r] - gi_mb(gv.x));
       }
     }
     GK_MARK(L, 6);
