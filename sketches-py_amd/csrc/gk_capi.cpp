@@ -73,6 +73,7 @@ struct gk_set {
   int32_t* d_ovf_count = nullptr;
   int32_t* d_ovf_list = nullptr;
   int64_t* d_zero_offs = nullptr;  // S+1 zeros: offsets of flush-only launches
+  unsigned long long* d_work = nullptr;  // stream hand-out counter of the small-class kernel
   // scratch
   double* d_qs = nullptr;
   int qs_alloc = 0;
@@ -212,7 +213,7 @@ int check_set(const gk_set* h) {
 hipError_t launch_class(gk_set* h, int c, const double* x, const int64_t* offs, const int32_t* list, int64_t count,
                         int force, const GKQuery& q, hipStream_t stream) {
   return gk_launch_ingest(h->st.cap[c], h->vpl, h->st, x, offs, list, count, force, h->d_ws, h->ws_bytes,
-                          h->ws_blocks, h->d_ovf_count, h->d_ovf_list, q, stream);
+                          h->ws_blocks, h->d_ovf_count, h->d_ovf_list, q, h->d_work, stream);
 }
 
 // Launch the ingest/flush kernel over every stream (class 0 over all, each
@@ -381,6 +382,7 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
   okm &= hipMalloc(&h->d_ovf_count, sizeof(int32_t)) == hipSuccess;
   okm &= hipMalloc(&h->d_ovf_list, S * sizeof(int32_t)) == hipSuccess;
   okm &= hipMalloc(&h->d_zero_offs, (S + 1) * sizeof(int64_t)) == hipSuccess;
+  okm &= hipMalloc(&h->d_work, GK_WORK_BYTES) == hipSuccess;
   if (!okm) {
     gk_destroy(h);
     return fail(GK_E_NOMEM, "device allocation for %lld streams failed", (long long)num_streams);
@@ -408,7 +410,7 @@ int gk_destroy(gk_set* h) {
   void* ptrs[] = {st.n,       st.E,           st.pend,          st.mn,          st.mx,         st.sum,
                   st.avg,     st.cls,         st.slot,          st.tab[0],      st.tab[1],     st.tab[2],
                   st.pbuf,    h->d_list[0],   h->d_list[1],     h->d_list[2],   h->d_qs,       h->d_ovf_count,
-                  h->d_ovf_list, h->d_tmp_list, h->d_tmp_slots, h->d_ws, h->d_zero_offs};
+                  h->d_ovf_list, h->d_tmp_list, h->d_tmp_slots, h->d_ws, h->d_zero_offs, h->d_work};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (auto& e : h->ev)

@@ -1408,21 +1408,46 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
                                                      const int32_t* __restrict__ list, int64_t count, int force,
                                                      int32_t* __restrict__ ovf_count, int32_t* __restrict__ ovf_list,
                                                      const double* __restrict__ qs, int nq,
-                                                     double* __restrict__ qout, int qmode) {
+                                                     double* __restrict__ qout, int qmode,
+                                                     unsigned long long* __restrict__ work) {
   __shared__ __attribute__((aligned(16))) SmallLDS<VPL> L;
   const int lane = threadIdx.x;
   const int P = st.P;
-  const int64_t G = gridDim.x;
 #ifdef GK_PROF
   if (lane == 0) {
     for (int i = 0; i < GK_PROF_NSEC; ++i) L.prof[i] = 0;
     L.prof_t = gk_cycles();
   }
 #endif
+  // Streams are handed out dynamically (one atomic per stream on `work`,
+  // zeroed before the launch), so waves on slower CUs simply take fewer
+  // streams; the next stream's id and header are fetched one stream ahead.
   GKHdrV hv;
-  if ((int64_t)blockIdx.x < count) gk_hdr_issue(hv, st, offs, list ? (int64_t)list[blockIdx.x] : (int64_t)blockIdx.x);
-  for (int64_t w = blockIdx.x; w < count; w += G) {
+#ifndef GK_WORK_PARTS
+#define GK_WORK_PARTS 8  // counters (one 128-B line each); a wave uses blockIdx % parts
+#endif
+#ifndef GK_WORK_CHUNK
+#define GK_WORK_CHUNK 2  // streams per grab
+#endif
+  const int nparts = (int)min((unsigned)GK_WORK_PARTS, gridDim.x);  // every part has a wave
+  const int part = (int)(blockIdx.x % (unsigned)nparts);
+  const int64_t pbeg = count * part / nparts, pend = count * (part + 1) / nparts;
+  int64_t cur = 0, cend = 0;
+  auto grab = [&]() -> int64_t {
+    if (cur >= cend) {
+      unsigned long long v = 0;
+      if (lane == 0) v = atomicAdd(work + 16 * part, (unsigned long long)GK_WORK_CHUNK);
+      cur = pbeg + rfl64((int64_t)v);
+      cend = min(cur + GK_WORK_CHUNK, pend);
+      if (cur >= pend) return count;
+    }
+    return cur++;
+  };
+  int64_t w = grab();
+  if (w < count) gk_hdr_issue(hv, st, offs, list ? (int64_t)list[w] : w);
+  for (; w < count;) {
     const int64_t s = list ? (int64_t)list[w] : w;
+    const int64_t wn = grab();
     const int32_t scls = __builtin_amdgcn_readfirstlane(hv.cls);
     const int32_t sslot = __builtin_amdgcn_readfirstlane(hv.slot);
     int p = __builtin_amdgcn_readfirstlane(hv.pend);
@@ -1432,7 +1457,8 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
     const int64_t xe = rfl64(hv.xe);
     const double smn = __longlong_as_double(rfl64(__double_as_longlong(hv.mn)));
     const double smx = __longlong_as_double(rfl64(__double_as_longlong(hv.mx)));
-    if (w + G < count) gk_hdr_issue(hv, st, offs, list ? (int64_t)list[w + G] : w + G);
+    if (wn < count) gk_hdr_issue(hv, st, offs, list ? (int64_t)list[wn] : wn);
+    w = wn;
     if (!list && scls != 0) continue;  // promoted: handled by its class launch
     const int64_t Lx = xe - xo;
     // force 1: flush only if values are pending (size/quantile, gk:45, 166, 197)
@@ -2007,16 +2033,20 @@ static hipError_t launch_ingest_vpl(int vpl, const GKState& st, const double* x,
 template <int VPL>
 static hipError_t launch_ingest_small(const GKState& st, const double* x, const int64_t* offs, const int32_t* list,
                                       int64_t count, int force, int32_t* ovf_count, int32_t* ovf_list,
-                                      const GKQuery& q, hipStream_t stream) {
+                                      const GKQuery& q, unsigned long long* work, hipStream_t stream) {
   if (count <= 0) return hipSuccess;
+  if (!work) return hipErrorInvalidValue;
   int occ = 0;
   (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_ingest_small<VPL>, 64, 0);
   if (occ <= 0) occ = 1;
-  int64_t grid = (int64_t)num_cu() * occ * 4;
+  // one resident wave per slot; streams are handed out through `work`
+  int64_t grid = (int64_t)num_cu() * occ;
   if (grid > count) grid = count;
   if (grid < 1) grid = 1;
+  hipError_t e = hipMemsetAsync(work, 0, GK_WORK_BYTES, stream);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL((k_ingest_small<VPL>), dim3((unsigned)grid), dim3(64), 0, stream, st, x, offs, list, count,
-                     force, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode);
+                     force, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode, work);
   return hipGetLastError();
 }
 
@@ -2025,11 +2055,11 @@ size_t gk_ingest_ws_bytes(int cap, int vpl) { return gk_flush_ws_bytes(cap, vpl)
 hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x, const int64_t* offs,
                             const int32_t* list, int64_t count, int force, unsigned char* ws, size_t ws_bytes,
                             int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list, const GKQuery& q,
-                            hipStream_t stream) {
+                            unsigned long long* work, hipStream_t stream) {
   switch (cap) {
     case SMALL_CAP:
-      if (vpl == 1) return launch_ingest_small<1>(st, x, offs, list, count, force, ovf_count, ovf_list, q, stream);
-      if (vpl == 2) return launch_ingest_small<2>(st, x, offs, list, count, force, ovf_count, ovf_list, q, stream);
+      if (vpl == 1) return launch_ingest_small<1>(st, x, offs, list, count, force, ovf_count, ovf_list, q, work, stream);
+      if (vpl == 2) return launch_ingest_small<2>(st, x, offs, list, count, force, ovf_count, ovf_list, q, work, stream);
       return hipErrorInvalidValue;
     case 2048:
       return launch_ingest_vpl<2048>(vpl, st, x, offs, list, count, force, cap, nullptr, 0, 0, ovf_count, ovf_list,

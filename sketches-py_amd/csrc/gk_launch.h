@@ -40,11 +40,13 @@ struct MergeArgsHost {
 
 int gk_num_cu();
 size_t gk_ingest_ws_bytes(int cap, int vpl);
-// cap 256 / 2048: LDS kernels; any other cap: global workspace ws (ws_bytes per block, ws_blocks blocks)
+#define GK_WORK_BYTES 1024  // 8 counters, one 128-byte line each
+// `work`: GK_WORK_BYTES of device counters of the small-class launch (dynamic stream hand-out).
+// cap GK_SMALL_CAP / 2048: LDS kernels; any other cap: global workspace ws (ws_bytes per block, ws_blocks blocks)
 hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x, const int64_t* offs,
                             const int32_t* list, int64_t count, int force, unsigned char* ws, size_t ws_bytes,
                             int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list, const GKQuery& q,
-                            hipStream_t stream);
+                            unsigned long long* work, hipStream_t stream);
 hipError_t gk_launch_stats(const GKState& st, const double* x, const int64_t* offs, hipStream_t stream);
 size_t gk_merge_lds_bytes(int cap, int pmax);
 hipError_t gk_launch_merge(const MergeArgsHost& h, hipStream_t stream);
