@@ -241,7 +241,22 @@ __global__ __launch_bounds__(256) void k_stats(GKState st, const double* __restr
         rv[r] = (i < so[min(ls + 1, nstr)]) ? x[i] : 0.0;
       }
     }
-    if (t < nstr) {
+    if (t < nstr && L - k0 >= STATS_CHUNK) {
+      // a full chunk: the reciprocals 1.0/n (IEEE divisions, off the chain)
+      // first, then the dependent _sum/_avg chain, fully unrolled
+      double rc[STATS_CHUNK];
+#pragma unroll
+      for (int k = 0; k < STATS_CHUNK; ++k) rc[k] = 1.0 / (double)(n + 1 + k);
+#pragma unroll
+      for (int k = 0; k < STATS_CHUNK; ++k) {
+        const double v = tile[t * STATS_ROW + k];
+        sm = sm + v;                              // gk:53
+        av = av + (v - av) * rc[k];               // gk:54 (no FMA: -ffp-contract=off)
+        if (v < mn) mn = v;                       // gk:56-57 (strict: first occurrence kept)
+        if (v > mx) mx = v;                       // gk:58-59
+      }
+      n += STATS_CHUNK;                           // gk:52
+    } else if (t < nstr) {
       const int kmax = (int)min((int64_t)STATS_CHUNK, L - k0);
       for (int k = 0; k < kmax; ++k) {
         const double v = tile[t * STATS_ROW + k];
@@ -962,6 +977,12 @@ struct SmallLDS {
 #endif
 };
 
+// gap counters of the next flush (read and written only inside a flush)
+__device__ __forceinline__ void small_zero_counts(uint32_t* gpk, int lane) {
+  if constexpr (SMALL_CAP == 128) *(uint2*)&gpk[2 * lane] = make_uint2(0u, 0u);
+  else for (int j = 4 * lane; j < SMALL_CAP; j += 256) *(uint4*)&gpk[j] = make_uint4(0u, 0u, 0u, 0u);
+}
+
 __device__ __forceinline__ void small_pad(double* tv, int E, int lane) {
   const int hi = gk_pow2_above(E) - 1;
   for (int j = E + lane; j < hi; j += 64) tv[pidx(j)] = __longlong_as_double(0x7ff0000000000000LL);
@@ -1064,32 +1085,10 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
   after_search();
   GK_MARK(L, 1);
 
-  // ---- gap counts and each value's slot in its gap ------------------------
-  const int j0 = lane * K;
-  if constexpr (K == 2) *(uint2*)&L.gpk[j0] = make_uint2(0u, 0u);
-  else *(uint4*)&L.gpk[j0] = make_uint4(0u, 0u, 0u, 0u);
-  wsync<false>();
-  uint32_t xs[VPL];
-#pragma unroll
-  for (int r = 0; r < VPL; ++r) xs[r] = (lane + 64 * r < cnt) ? atomicAdd(&L.gpk[xg[r]], 1u) : 0u;
-  wsync<false>();
-  uint32_t mloc = 0;
-#pragma unroll
-  for (int r = 0; r < VPL; ++r) mloc = max(mloc, xs[r] + 1u);
-  // +0.0 and -0.0 in one flush: only the exact (insertion-index) tie-break
-  // of the counting path orders them like the reference
-  bool pz = false, nz = false;
-#pragma unroll
-  for (int r = 0; r < VPL; ++r) {
-    const bool z = (lane + 64 * r < cnt) && xv[r] == 0.0;
-    pz |= z && !signbit(xv[r]);
-    nz |= z && signbit(xv[r]);
-  }
-  const bool use_sort = (wave_max_u32(mloc) > GK_SMALL_RANK_MAX) ||
-                        (__builtin_amdgcn_ballot_w64(pz) != 0 && __builtin_amdgcn_ballot_w64(nz) != 0);
-  GK_MARK(L, 2);
-
   // ---- the lane's K entries (+ successor) into registers ------------------
+  // (the table is not written before the scan below: these reads are issued
+  // beside the count atomics instead of after them)
+  const int j0 = lane * K;
   double ev[K];
   int eg[K + 1], ed[K + 1], em[K];
   {
@@ -1116,6 +1115,29 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
       ed[e] = v ? gd[e].y : 0;
     }
   }
+
+  // ---- gap counts and each value's slot in its gap ------------------------
+  // (the counters were zeroed at the end of the previous flush / stream setup)
+  uint32_t xs[VPL];
+#pragma unroll
+  for (int r = 0; r < VPL; ++r) xs[r] = (lane + 64 * r < cnt) ? atomicAdd(&L.gpk[xg[r]], 1u) : 0u;
+  wsync<false>();
+  uint32_t mloc = 0;
+#pragma unroll
+  for (int r = 0; r < VPL; ++r) mloc = max(mloc, xs[r] + 1u);
+  // +0.0 and -0.0 in one flush: only the exact (insertion-index) tie-break
+  // of the counting path orders them like the reference
+  bool pz = false, nz = false;
+#pragma unroll
+  for (int r = 0; r < VPL; ++r) {
+    const bool z = (lane + 64 * r < cnt) && xv[r] == 0.0;
+    pz |= z && !signbit(xv[r]);
+    nz |= z && signbit(xv[r]);
+  }
+  const bool use_sort = (__builtin_amdgcn_ballot_w64(mloc > (uint32_t)GK_SMALL_RANK_MAX) != 0) ||
+                        (__builtin_amdgcn_ballot_w64(pz) != 0 && __builtin_amdgcn_ballot_w64(nz) != 0);
+  GK_MARK(L, 2);
+
   {
     uint32_t mm[K];
     if constexpr (K == 2) {
@@ -1225,7 +1247,7 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
     // signs of zero takes the exact path below, so the output is the same.
     int2 gv[VPL];
     int gb[VPL], mo[VPL], me[VPL];
-    uint32_t omax = 0;
+    int omax = 0;  // this lane's largest member count; the loop runs while any lane needs it
 #pragma unroll
     for (int r = 0; r < VPL; ++r) {
       const bool v = lane + 64 * r < cnt;
@@ -1236,14 +1258,13 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
       mo[r] = v ? ge - gb[r] - 1 : 0;  // other members of the gap
       me[r] = (int)xs[r];
       if (v) L.mv[gb[r] + me[r]] = xv[r];
-      omax = max(omax, (uint32_t)mo[r]);
+      omax = max(omax, mo[r]);
     }
-    omax = wave_max_u32(omax);
     wsync<false>();
     int rk[VPL];
 #pragma unroll
     for (int r = 0; r < VPL; ++r) rk[r] = 0;
-    for (int u0 = 0; u0 < (int)omax; u0 += 2) {
+    for (int u0 = 0; __builtin_amdgcn_ballot_w64(u0 < omax) != 0; u0 += 2) {
       double y[VPL][2];
 #pragma unroll
       for (int r = 0; r < VPL; ++r)
@@ -1322,6 +1343,7 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
     GK_MARK(L, 6);
   }
   small_pad(L.tv, newE, lane);
+  small_zero_counts(L.gpk, lane);
   wsync<false>();
   GK_MARK(L, 7);
   return newE;
@@ -1484,6 +1506,7 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
         }
       }
       small_pad(L.tv, E, lane);
+      small_zero_counts(L.gpk, lane);
     }
     wsync<false>();
     GK_MARK(L, 0);
