@@ -74,6 +74,8 @@ struct gk_set {
   int32_t* d_ovf_list = nullptr;
   int64_t* d_zero_offs = nullptr;  // S+1 zeros: offsets of flush-only launches
   unsigned long long* d_work = nullptr;  // stream hand-out counter of the small-class kernel
+  int32_t* d_long_list = nullptr;        // streams k_stats hands to k_stats_long
+  int32_t* d_long_count = nullptr;
   // scratch
   double* d_qs = nullptr;
   int qs_alloc = 0;
@@ -383,6 +385,8 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
   okm &= hipMalloc(&h->d_ovf_list, S * sizeof(int32_t)) == hipSuccess;
   okm &= hipMalloc(&h->d_zero_offs, (S + 1) * sizeof(int64_t)) == hipSuccess;
   okm &= hipMalloc(&h->d_work, GK_WORK_BYTES) == hipSuccess;
+  okm &= hipMalloc(&h->d_long_list, S * sizeof(int32_t)) == hipSuccess;
+  okm &= hipMalloc(&h->d_long_count, sizeof(int32_t)) == hipSuccess;
   if (!okm) {
     gk_destroy(h);
     return fail(GK_E_NOMEM, "device allocation for %lld streams failed", (long long)num_streams);
@@ -410,7 +414,8 @@ int gk_destroy(gk_set* h) {
   void* ptrs[] = {st.n,       st.E,           st.pend,          st.mn,          st.mx,         st.sum,
                   st.avg,     st.cls,         st.slot,          st.tab[0],      st.tab[1],     st.tab[2],
                   st.pbuf,    h->d_list[0],   h->d_list[1],     h->d_list[2],   h->d_qs,       h->d_ovf_count,
-                  h->d_ovf_list, h->d_tmp_list, h->d_tmp_slots, h->d_ws, h->d_zero_offs, h->d_work};
+                  h->d_ovf_list, h->d_tmp_list, h->d_tmp_slots, h->d_ws, h->d_zero_offs, h->d_work,
+                  h->d_long_list, h->d_long_count};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (auto& e : h->ev)
@@ -443,7 +448,7 @@ int gk_ingest(gk_set* h, const double* values, const int64_t* offsets, void* str
   if (h->S == 0) return GK_OK;
   hipStream_t s = (hipStream_t)stream;
   if (h->timing) HIP_TRY(hipEventRecord(h->ev[2], s));
-  HIP_TRY(gk_launch_stats(h->st, values, offsets, s));
+  HIP_TRY(gk_launch_stats(h->st, values, offsets, h->d_long_list, h->d_long_count, s));
   if (h->timing) HIP_TRY(hipEventRecord(h->ev[3], s));
   rc = run_ingest(h, values, offsets, 0, s);
   if (rc) return rc;
@@ -521,7 +526,7 @@ int gk_ingest_quantiles(gk_set* h, const double* values, const int64_t* offsets,
   if (h->S == 0) return GK_OK;
   if (nq == 0) return gk_ingest(h, values, offsets, stream);
   if (h->timing) HIP_TRY(hipEventRecord(h->ev[2], s));
-  HIP_TRY(gk_launch_stats(h->st, values, offsets, s));
+  HIP_TRY(gk_launch_stats(h->st, values, offsets, h->d_long_list, h->d_long_count, s));
   if (h->timing) HIP_TRY(hipEventRecord(h->ev[3], s));
   // add every value (gk:49-61), then quantiles() (gk:187-232): flush the
   // leftover pending values and answer from the LDS-resident table

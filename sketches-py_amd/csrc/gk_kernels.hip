@@ -184,10 +184,14 @@ __device__ __forceinline__ GKRec* gk_table_ptr_cs(const GKState& st, int64_t s, 
 // pre-call n.
 // ===========================================================================
 #define STATS_CHUNK 16
+#ifndef GK_STATS_LONG
+#define GK_STATS_LONG 16384  // longer streams go to k_stats_long (one wave each)
+#endif
 #define STATS_ROW (STATS_CHUNK + 1)  // +1 double: lanes' rows start on different banks
 
 __global__ __launch_bounds__(256) void k_stats(GKState st, const double* __restrict__ x,
-                                               const int64_t* __restrict__ offs) {
+                                               const int64_t* __restrict__ offs,
+                                               int32_t* __restrict__ long_list, int32_t* __restrict__ long_count) {
   __shared__ double tile[256 * STATS_ROW];
   __shared__ int64_t so[257];
   __shared__ int64_t smax;
@@ -202,6 +206,10 @@ __global__ __launch_bounds__(256) void k_stats(GKState st, const double* __restr
   __syncthreads();
   int64_t L = 0;
   if (t < nstr) L = so[t + 1] - so[t];
+  if (L > GK_STATS_LONG) {  // walked by k_stats_long, not in this block's trip count
+    long_list[atomicAdd(long_count, 1)] = (int32_t)(s0 + t);
+    L = 0;
+  }
   // block-uniform trip count: the longest stream of the block
   atomicMax((unsigned long long*)&smax, (unsigned long long)L);
   __syncthreads();
@@ -274,6 +282,92 @@ __global__ __launch_bounds__(256) void k_stats(GKState st, const double* __restr
     st.mx[s] = mx;
     st.sum[s] = sm;
     st.avg[s] = av;
+  }
+}
+
+// ===========================================================================
+// k_stats_long: gk:52-59 for the streams k_stats hands over (longer than
+// GK_STATS_LONG values), one wave per stream.  The _avg update is three
+// dependent float64 roundings per value, so a long stream's chain latency
+// sets the time: the wave keeps SL_DEPTH chunks of 64 values in flight
+// (coalesced loads), each lane computes the reciprocal 1.0/n of its value off
+// the chain, and every lane walks the chain over LDS broadcast reads of
+// (v, 1/n) -- identical results in every lane, lane 0 writes them.
+// _min/_max: each lane's first occurrence, reduced by (value, index), then
+// folded into the pre-call values with the strict compares of gk:56-59.
+// ===========================================================================
+#define SL_DEPTH 4
+
+__global__ __launch_bounds__(64) void k_stats_long(GKState st, const double* __restrict__ x,
+                                                   const int64_t* __restrict__ offs,
+                                                   const int32_t* __restrict__ list,
+                                                   const int32_t* __restrict__ count) {
+  __shared__ double2 buf[64];
+  const int lane = threadIdx.x;
+  const int cnt = *count;
+  for (int w = blockIdx.x; w < cnt; w += gridDim.x) {
+    const int64_t s = list[w];
+    const int64_t xo = offs[s];
+    const int64_t L = offs[s + 1] - xo;
+    int64_t n = st.n[s];  // pre-call n: k_ingest runs after this kernel on the same HIP stream
+    double sm = st.sum[s], av = st.avg[s];
+    double lmn = __longlong_as_double(0x7ff0000000000000LL), lmx = -lmn;
+    int64_t imn = INT64_MAX, imx = INT64_MAX;
+    double q[SL_DEPTH];
+#pragma unroll
+    for (int d = 0; d < SL_DEPTH; ++d) q[d] = (64 * d + lane < L) ? x[xo + 64 * d + lane] : 0.0;
+    for (int64_t k0 = 0; k0 < L; k0 += 64 * SL_DEPTH) {
+#pragma unroll
+      for (int d = 0; d < SL_DEPTH; ++d) {
+        const int64_t c0 = k0 + 64 * d;  // first index of this chunk
+        if (c0 < L) {
+          const int cn = (int)min((int64_t)64, L - c0);
+          const double v = q[d];
+          if (lane < cn) {
+            const int64_t idx = c0 + lane;
+            if (v < lmn) { lmn = v; imn = idx; }
+            if (v > lmx) { lmx = v; imx = idx; }
+          }
+          buf[lane] = make_double2(v, 1.0 / (double)(n + 1 + lane));
+          const int64_t nx = c0 + 64 * SL_DEPTH + lane;  // refill: the chunk SL_DEPTH ahead
+          q[d] = (nx < L) ? x[xo + nx] : 0.0;
+          wsync<false>();
+          if (cn == 64) {
+#pragma unroll 8
+            for (int j = 0; j < 64; ++j) {
+              const double2 e = buf[j];
+              sm = sm + e.x;                    // gk:53
+              av = av + (e.x - av) * e.y;       // gk:54
+            }
+          } else {
+            for (int j = 0; j < cn; ++j) {
+              const double2 e = buf[j];
+              sm = sm + e.x;
+              av = av + (e.x - av) * e.y;
+            }
+          }
+          n += cn;  // gk:52
+          wsync<false>();
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double omn = __shfl_xor(lmn, o, 64), omx = __shfl_xor(lmx, o, 64);
+      const int64_t oin = __shfl_xor(imn, o, 64), oix = __shfl_xor(imx, o, 64);
+      if (omn < lmn || (omn == lmn && oin < imn)) { lmn = omn; imn = oin; }
+      if (omx > lmx || (omx == lmx && oix < imx)) { lmx = omx; imx = oix; }
+    }
+    if (lane == 0) {
+      double mn = st.mn[s], mx = st.mx[s];
+      if (lmn < mn) mn = lmn;  // gk:56-57: the pre-call value wins ties
+      if (lmx > mx) mx = lmx;  // gk:58-59
+      st.mn[s] = mn;
+      st.mx[s] = mx;
+      st.sum[s] = sm;
+      st.avg[s] = av;
+    }
+    wsync<false>();
   }
 }
 
@@ -2094,10 +2188,17 @@ hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x
   }
 }
 
-hipError_t gk_launch_stats(const GKState& st, const double* x, const int64_t* offs, hipStream_t stream) {
+hipError_t gk_launch_stats(const GKState& st, const double* x, const int64_t* offs, int32_t* long_list,
+                           int32_t* long_count, hipStream_t stream) {
   if (st.S <= 0) return hipSuccess;
+  hipError_t e = hipMemsetAsync(long_count, 0, sizeof(int32_t), stream);
+  if (e != hipSuccess) return e;
   const int64_t grid = (st.S + 255) / 256;
-  hipLaunchKernelGGL(k_stats, dim3((unsigned)grid), dim3(256), 0, stream, st, x, offs);
+  hipLaunchKernelGGL(k_stats, dim3((unsigned)grid), dim3(256), 0, stream, st, x, offs, long_list, long_count);
+  // the long-stream count is only known on the device: a fixed grid of waves
+  // reads it (an empty list costs one short launch)
+  hipLaunchKernelGGL(k_stats_long, dim3((unsigned)(num_cu() * 4)), dim3(64), 0, stream, st, x, offs,
+                     (const int32_t*)long_list, (const int32_t*)long_count);
   return hipGetLastError();
 }
 

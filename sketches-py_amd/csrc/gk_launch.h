@@ -47,7 +47,9 @@ hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x
                             const int32_t* list, int64_t count, int force, unsigned char* ws, size_t ws_bytes,
                             int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list, const GKQuery& q,
                             unsigned long long* work, hipStream_t stream);
-hipError_t gk_launch_stats(const GKState& st, const double* x, const int64_t* offs, hipStream_t stream);
+// long_list (S entries) / long_count: device scratch for the streams handed to k_stats_long
+hipError_t gk_launch_stats(const GKState& st, const double* x, const int64_t* offs, int32_t* long_list,
+                           int32_t* long_count, hipStream_t stream);
 size_t gk_merge_lds_bytes(int cap, int pmax);
 hipError_t gk_launch_merge(const MergeArgsHost& h, hipStream_t stream);
 hipError_t gk_launch_reset(const GKState& st, hipStream_t stream);

@@ -378,3 +378,23 @@ def test_fused_ingest_quantiles_vs_oracle(gpu_device):
             exp = osx.quantiles(qs, single=single)
             assert_same_quantiles(got.cpu().numpy(), exp, "fused eps=%g qs=%r" % (eps, qs))
             assert_same_state(ss, osx, "fused state eps=%g" % eps)
+
+
+def test_long_stream_stats(gpu_device):
+    """Streams longer than GK_STATS_LONG (16384) take k_stats_long: _sum/_avg
+    chain and first-occurrence _min/_max (signed zeros) across calls."""
+    rng = np.random.default_rng(41)
+    lens = [16385, 20000, 70001, 100, 0, 33333]
+    dists = [6, 1, 6, 6, 0, 7]
+    S = len(lens)
+    for eps in (0.01, 0.001):
+        ss = _ss(S, eps, gpu_device)
+        osx = OracleSet(S, eps)
+        for part in range(2):
+            seqs = [gen(d, L // (part + 1), rng) for d, L in zip(dists, lens)]
+            flat, offs = csr(seqs)
+            ss.ingest(torch.from_numpy(flat), torch.from_numpy(offs))
+            osx.ingest(flat, offs)
+            assert_same_state(ss, osx, "long eps=%g part %d" % (eps, part))
+        got = ss.quantiles([0.5, 0.9, 0.99]).cpu().numpy()
+        assert_same_quantiles(got, osx.quantiles([0.5, 0.9, 0.99]), "long q eps=%g" % eps)
