@@ -74,8 +74,13 @@ struct gk_set {
   int32_t* d_ovf_list = nullptr;
   int64_t* d_zero_offs = nullptr;  // S+1 zeros: offsets of flush-only launches
   unsigned long long* d_work = nullptr;  // stream hand-out counter of the small-class kernel
-  int32_t* d_long_list = nullptr;        // streams k_stats hands to k_stats_long
+  int32_t* d_long_list = nullptr;        // streams k_stats hands to k_stats_long (longest first)
+  int64_t* d_long_n = nullptr;           //   and their pre-call n
   int32_t* d_long_count = nullptr;
+  // k_stats_long (the sequential _sum/_avg chains of long streams) runs on
+  // this stream beside the ingest launches; ev_fork / ev_join order it
+  hipStream_t aux = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // scratch
   double* d_qs = nullptr;
   int qs_alloc = 0;
@@ -213,22 +218,51 @@ int check_set(const gk_set* h) {
 }
 
 hipError_t launch_class(gk_set* h, int c, const double* x, const int64_t* offs, const int32_t* list, int64_t count,
-                        int force, const GKQuery& q, hipStream_t stream) {
+                        int force, const GKQuery& q, hipStream_t stream, bool prio = false) {
   return gk_launch_ingest(h->st.cap[c], h->vpl, h->st, x, offs, list, count, force, h->d_ws, h->ws_bytes,
-                          h->ws_blocks, h->d_ovf_count, h->d_ovf_list, q, h->d_work, stream);
+                          h->ws_blocks, h->d_ovf_count, h->d_ovf_list, q, h->d_work,
+                          prio ? h->d_long_list : nullptr, prio ? h->d_long_count : nullptr, stream);
+}
+
+// gk:52-59 for a batch: k_stats over every stream on `s` (it lists the
+// streams longer than GK_STATS_LONG values, longest first), then the long
+// streams' sequential _sum/_avg chains on h->aux, beside the ingest launches
+// that follow on `s` (they touch neither _sum nor _avg).  stats_join makes
+// `s` wait for them and, for a fused query, re-answers the long streams with
+// their final _min/_max.
+int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s) {
+  if (h->timing) HIP_TRY(hipEventRecord(h->ev[2], s));
+  HIP_TRY(gk_launch_stats(h->st, x, offs, h->d_long_list, h->d_long_n, h->d_long_count, s));
+  if (h->timing) HIP_TRY(hipEventRecord(h->ev[3], s));
+  HIP_TRY(hipEventRecord(h->ev_fork, s));
+  HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_fork, 0));
+  HIP_TRY(gk_launch_stats_long(h->st, x, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->aux));
+  HIP_TRY(hipEventRecord(h->ev_join, h->aux));
+  return GK_OK;
+}
+
+int stats_join(gk_set* h, hipStream_t s, const GKQuery& q) {
+  HIP_TRY(hipStreamWaitEvent(s, h->ev_join, 0));
+  HIP_TRY(gk_launch_query_list(h->st, h->d_long_list, h->d_long_count, q, s));
+  if (h->timing) {
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, h->ev[2], h->ev[3]));
+    h->stats_ms += ms;
+  }
+  return GK_OK;
 }
 
 // Launch the ingest/flush kernel over every stream (class 0 over all, each
 // larger class over its member list); streams that overflow their class were
 // not committed, so they are promoted one class up and run again.
 int run_ingest(gk_set* h, const double* x, const int64_t* offs, int force, hipStream_t stream,
-               const GKQuery& q = GKQuery()) {
+               const GKQuery& q = GKQuery(), bool prio = false) {
   if (!offs) offs = h->d_zero_offs;
   HIP_TRY(hipMemsetAsync(h->d_ovf_count, 0, sizeof(int32_t), stream));
   // timing covers the class-0 batch launch of gk_ingest (force == 0) only
   const bool timed = h->timing && x != nullptr;
   if (timed) HIP_TRY(hipEventRecord(h->ev[0], stream));
-  HIP_TRY(launch_class(h, 0, x, offs, nullptr, h->S, force, q, stream));
+  HIP_TRY(launch_class(h, 0, x, offs, nullptr, h->S, force, q, stream, prio && x != nullptr));
   if (timed) HIP_TRY(hipEventRecord(h->ev[1], stream));
   for (int c = 1; c < h->st.nclass; ++c)
     if (!h->members[c].empty())
@@ -386,7 +420,11 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
   okm &= hipMalloc(&h->d_zero_offs, (S + 1) * sizeof(int64_t)) == hipSuccess;
   okm &= hipMalloc(&h->d_work, GK_WORK_BYTES) == hipSuccess;
   okm &= hipMalloc(&h->d_long_list, S * sizeof(int32_t)) == hipSuccess;
+  okm &= hipMalloc(&h->d_long_n, S * sizeof(int64_t)) == hipSuccess;
   okm &= hipMalloc(&h->d_long_count, sizeof(int32_t)) == hipSuccess;
+  okm &= hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking) == hipSuccess;
+  okm &= hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) == hipSuccess;
+  okm &= hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) == hipSuccess;
   if (!okm) {
     gk_destroy(h);
     return fail(GK_E_NOMEM, "device allocation for %lld streams failed", (long long)num_streams);
@@ -410,16 +448,20 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
 
 int gk_destroy(gk_set* h) {
   if (!h) return GK_OK;
+  if (h->aux) (void)hipStreamSynchronize(h->aux);  // k_stats_long may still read the set
   GKState& st = h->st;
   void* ptrs[] = {st.n,       st.E,           st.pend,          st.mn,          st.mx,         st.sum,
                   st.avg,     st.cls,         st.slot,          st.tab[0],      st.tab[1],     st.tab[2],
                   st.pbuf,    h->d_list[0],   h->d_list[1],     h->d_list[2],   h->d_qs,       h->d_ovf_count,
                   h->d_ovf_list, h->d_tmp_list, h->d_tmp_slots, h->d_ws, h->d_zero_offs, h->d_work,
-                  h->d_long_list, h->d_long_count};
+                  h->d_long_list, h->d_long_n, h->d_long_count};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (auto& e : h->ev)
     if (e) (void)hipEventDestroy(e);
+  if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+  if (h->ev_join) (void)hipEventDestroy(h->ev_join);
+  if (h->aux) (void)hipStreamDestroy(h->aux);
   delete h;
   return GK_OK;
 }
@@ -447,17 +489,11 @@ int gk_ingest(gk_set* h, const double* values, const int64_t* offsets, void* str
   if (!values) return fail(GK_E_ARG, "values is null");
   if (h->S == 0) return GK_OK;
   hipStream_t s = (hipStream_t)stream;
-  if (h->timing) HIP_TRY(hipEventRecord(h->ev[2], s));
-  HIP_TRY(gk_launch_stats(h->st, values, offsets, h->d_long_list, h->d_long_count, s));
-  if (h->timing) HIP_TRY(hipEventRecord(h->ev[3], s));
-  rc = run_ingest(h, values, offsets, 0, s);
+  rc = stats_fork(h, values, offsets, s);
   if (rc) return rc;
-  if (h->timing) {
-    float ms = 0;
-    HIP_TRY(hipEventElapsedTime(&ms, h->ev[2], h->ev[3]));
-    h->stats_ms += ms;
-  }
-  return GK_OK;
+  rc = run_ingest(h, values, offsets, 0, s, GKQuery(), true);
+  const int rj = stats_join(h, s, GKQuery());  // joined on every path
+  return rc ? rc : rj;
 }
 
 int gk_flush(gk_set* h, void* stream) {
@@ -525,18 +561,14 @@ int gk_ingest_quantiles(gk_set* h, const double* values, const int64_t* offsets,
   if (rc) return rc;
   if (h->S == 0) return GK_OK;
   if (nq == 0) return gk_ingest(h, values, offsets, stream);
-  if (h->timing) HIP_TRY(hipEventRecord(h->ev[2], s));
-  HIP_TRY(gk_launch_stats(h->st, values, offsets, h->d_long_list, h->d_long_count, s));
-  if (h->timing) HIP_TRY(hipEventRecord(h->ev[3], s));
+  rc = stats_fork(h, values, offsets, s);
+  if (rc) return rc;
   // add every value (gk:49-61), then quantiles() (gk:187-232): flush the
   // leftover pending values and answer from the LDS-resident table
-  rc = run_ingest(h, values, offsets, 1, s, q);
+  rc = run_ingest(h, values, offsets, 1, s, q, true);
+  const int rj = stats_join(h, s, q);  // joined on every path
   if (rc) return rc;
-  if (h->timing) {
-    float ms = 0;
-    HIP_TRY(hipEventElapsedTime(&ms, h->ev[2], h->ev[3]));
-    h->stats_ms += ms;
-  }
+  if (rj) return rj;
   HIP_TRY(hipStreamSynchronize(s));
   return GK_OK;
 }

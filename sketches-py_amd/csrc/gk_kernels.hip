@@ -286,6 +286,59 @@ __global__ __launch_bounds__(256) void k_stats(GKState st, const double* __restr
 }
 
 // ===========================================================================
+// k_long_prep: the long-stream list k_stats built (in atomic order) sorted by
+// length, longest first (ties: lower stream id first), so that k_ingest and
+// k_stats_long start the longest sequential chains first; and the pre-call n
+// of every listed stream saved for k_stats_long, which runs beside k_ingest
+// (k_ingest rewrites n).  One 1024-thread block, bitonic sort of 64-bit keys
+// in LDS; lists longer than GK_SORT_LONG_MAX keep their arrival order (still
+// correct, only less balanced).  Runs before k_ingest on the same HIP stream.
+// ===========================================================================
+#define GK_SORT_LONG_MAX 4096
+
+__global__ __launch_bounds__(1024) void k_long_prep(GKState st, const int64_t* __restrict__ offs,
+                                                    int32_t* __restrict__ list, int64_t* __restrict__ list_n,
+                                                    const int32_t* __restrict__ count) {
+  __shared__ uint64_t key[GK_SORT_LONG_MAX];
+  const int cnt = *count;
+  const int t = threadIdx.x;
+  if (cnt > 1 && cnt <= GK_SORT_LONG_MAX) {
+    int N = 2;
+    while (N < cnt) N <<= 1;
+    constexpr uint64_t LMAX = (1ull << 33) - 1;
+    for (int i = t; i < N; i += 1024) {
+      uint64_t k = ~0ull;
+      if (i < cnt) {
+        const int64_t s = list[i];
+        uint64_t L = (uint64_t)(offs[s + 1] - offs[s]);
+        if (L > LMAX) L = LMAX;
+        // ascending key = descending length, then ascending stream id
+        k = ((LMAX - L) << 31) | (uint64_t)s;
+      }
+      key[i] = k;
+    }
+    __syncthreads();
+    for (int k = 2; k <= N; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int pp = t; pp < N / 2; pp += 1024) {
+          const int i = ((pp & ~(j - 1)) << 1) | (pp & (j - 1));
+          const int l = i + j;
+          const uint64_t a = key[i], b = key[l];
+          if ((a > b) == ((i & k) == 0)) {
+            key[i] = b;
+            key[l] = a;
+          }
+        }
+        __syncthreads();
+      }
+    }
+    for (int i = t; i < cnt; i += 1024) list[i] = (int32_t)(key[i] & 0x7fffffffu);
+    __syncthreads();
+  }
+  for (int i = t; i < cnt; i += 1024) list_n[i] = st.n[list[i]];
+}
+
+// ===========================================================================
 // k_stats_long: gk:52-59 for the streams k_stats hands over (longer than
 // GK_STATS_LONG values), one wave per stream.  The _avg update is three
 // dependent float64 roundings per value, so a long stream's chain latency
@@ -301,6 +354,7 @@ __global__ __launch_bounds__(256) void k_stats(GKState st, const double* __restr
 __global__ __launch_bounds__(64) void k_stats_long(GKState st, const double* __restrict__ x,
                                                    const int64_t* __restrict__ offs,
                                                    const int32_t* __restrict__ list,
+                                                   const int64_t* __restrict__ list_n,
                                                    const int32_t* __restrict__ count) {
   __shared__ double2 buf[64];
   const int lane = threadIdx.x;
@@ -309,7 +363,7 @@ __global__ __launch_bounds__(64) void k_stats_long(GKState st, const double* __r
     const int64_t s = list[w];
     const int64_t xo = offs[s];
     const int64_t L = offs[s + 1] - xo;
-    int64_t n = st.n[s];  // pre-call n: k_ingest runs after this kernel on the same HIP stream
+    int64_t n = list_n[w];  // pre-call n (k_ingest may already have rewritten st.n[s])
     double sm = st.sum[s], av = st.avg[s];
     double lmn = __longlong_as_double(0x7ff0000000000000LL), lmx = -lmn;
     int64_t imn = INT64_MAX, imx = INT64_MAX;
@@ -830,6 +884,25 @@ __device__ __attribute__((noinline)) void wave_quantiles(const double* __restric
   }
 }
 
+// k_query_list: quantiles (gk:156-232) of the listed streams from their
+// committed tables in HBM, one wave per stream.  The fused ingest+query
+// launch answers every stream before k_stats_long (running beside it) has
+// produced the final _min/_max of the long streams (gk:183, 220, 229); this
+// launch re-answers exactly those streams once it has joined.
+__global__ __launch_bounds__(64) void k_query_list(GKState st, const int32_t* __restrict__ list,
+                                                   const int32_t* __restrict__ count,
+                                                   const double* __restrict__ qs, int nq, int qmode,
+                                                   double* __restrict__ qout) {
+  const int lane = threadIdx.x;
+  const int cnt = *count;
+  for (int w = blockIdx.x; w < cnt; w += gridDim.x) {
+    const int64_t s = list[w];
+    const GKRec* tab = gk_table_ptr(st, s);
+    wave_quantiles<2, 4>(&tab->v, &tab->g, &tab->d, st.E[s], st.n[s], st.mn[s], st.mx[s], st, qs, nq, qmode,
+                         qout + s * (int64_t)nq, lane);
+  }
+}
+
 // CAP > 0: LDS working storage of that capacity (class 256 / 2048).
 // CAP == 0: global workspace `ws` (ws_bytes per block) of capacity `cap`.
 // list == NULL: every class-0 stream; else the listed streams (class c > 0).
@@ -840,7 +913,10 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
                                                int force, int cap, unsigned char* ws, size_t ws_bytes,
                                                int32_t* __restrict__ ovf_count,
                                                int32_t* __restrict__ ovf_list, const double* __restrict__ qs,
-                                               int nq, double* __restrict__ qout, int qmode) {
+                                               int nq, double* __restrict__ qout, int qmode,
+                                               unsigned long long* __restrict__ work,
+                                               const int32_t* __restrict__ prio,
+                                               const int32_t* __restrict__ prio_count) {
   constexpr int LCAP = CAP > 0 ? CAP : 1;
   constexpr int LVPL = CAP > 0 ? VPL : 1;
   __shared__ FlushLDS<LCAP, LVPL> Ls;
@@ -855,11 +931,29 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
   const int P = st.P;
   // headers are prefetched one stream ahead; flush-only launches pass
   // x == NULL and an all-zero offs array
-  const int64_t G = gridDim.x;
+  // Streams are handed out dynamically (one atomic per stream on `work`,
+  // zeroed before the launch).  Work items [0, npri) are the streams of
+  // `prio` -- the streams longer than GK_STATS_LONG values, longest first
+  // (k_sort_long) -- so that the long sequential flush chains start at once;
+  // items [npri, npri+count) are the launch's streams in order, minus those
+  // already taken from `prio` (the same length test k_stats applied).
+  const int64_t npri = prio ? (int64_t)*prio_count : 0;
+  const int64_t total = npri + count;
+  auto grab = [&]() -> int64_t {
+    unsigned long long v = 0;
+    if (lane == 0) v = atomicAdd(work, 1ull);
+    return rfl64((int64_t)v);
+  };
+  auto sid = [&](int64_t w) -> int64_t {
+    return w < npri ? (int64_t)prio[w] : (list ? (int64_t)list[w - npri] : w - npri);
+  };
   GKHdrV hv;
-  if ((int64_t)blockIdx.x < count) gk_hdr_issue(hv, st, offs, list ? (int64_t)list[blockIdx.x] : (int64_t)blockIdx.x);
-  for (int64_t w = blockIdx.x; w < count; w += G) {
-    const int64_t s = list ? (int64_t)list[w] : w;
+  int64_t w = grab();
+  if (w < total) gk_hdr_issue(hv, st, offs, sid(w));
+  for (; w < total;) {
+    const int64_t s = sid(w);
+    const bool from_prio = w < npri;
+    const int64_t wn = grab();
     const int32_t scls = __builtin_amdgcn_readfirstlane(hv.cls);
     const int32_t sslot = __builtin_amdgcn_readfirstlane(hv.slot);
     int p = __builtin_amdgcn_readfirstlane(hv.pend);
@@ -869,9 +963,11 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
     const int64_t xe = rfl64(hv.xe);
     const double smn = __longlong_as_double(rfl64(__double_as_longlong(hv.mn)));
     const double smx = __longlong_as_double(rfl64(__double_as_longlong(hv.mx)));
-    if (w + G < count) gk_hdr_issue(hv, st, offs, list ? (int64_t)list[w + G] : w + G);
+    if (wn < total) gk_hdr_issue(hv, st, offs, sid(wn));
+    w = wn;
     if (!list && scls != 0) continue;  // promoted: handled by its class launch
     const int64_t Lx = xe - xo;
+    if (prio && !from_prio && Lx > GK_STATS_LONG) continue;  // taken from `prio`
 
     // force 1: flush only if values are pending (size/quantile, gk:45, 166, 197)
     // force 2: unconditional merge_compress() (merge, gk:122, 126, 137)
@@ -2111,21 +2207,28 @@ template <int CAP, int VPL>
 static hipError_t launch_ingest_t(const GKState& st, const double* x, const int64_t* offs,
                                   const int32_t* list, int64_t count, int force, int cap,
                                   unsigned char* ws, size_t ws_bytes, int64_t ws_blocks,
-                                  int32_t* ovf_count, int32_t* ovf_list, const GKQuery& q, hipStream_t stream) {
+                                  int32_t* ovf_count, int32_t* ovf_list, const GKQuery& q,
+                                  unsigned long long* work, const int32_t* prio, const int32_t* prio_count,
+                                  hipStream_t stream) {
   if (count <= 0) return hipSuccess;
+  if (!work) return hipErrorInvalidValue;
   int64_t grid;
   if (CAP > 0) {
+    // one resident wave per slot; streams are handed out through `work`
     int occ = 0;
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_ingest<CAP, VPL>, 64, 0);
     if (occ <= 0) occ = 1;
-    grid = (int64_t)num_cu() * occ * 4;
+    grid = (int64_t)num_cu() * occ;
   } else {
     grid = ws_blocks;
   }
-  if (grid > count) grid = count;
+  if (!prio && grid > count) grid = count;
   if (grid < 1) grid = 1;
+  hipError_t e = hipMemsetAsync(work, 0, sizeof(unsigned long long), stream);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL((k_ingest<CAP, VPL>), dim3((unsigned)grid), dim3(64), 0, stream, st, x, offs, list,
-                     count, force, cap, ws, ws_bytes, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode);
+                     count, force, cap, ws, ws_bytes, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode, work,
+                     prio, prio_count);
   return hipGetLastError();
 }
 
@@ -2133,9 +2236,10 @@ template <int CAP>
 static hipError_t launch_ingest_vpl(int vpl, const GKState& st, const double* x, const int64_t* offs,
                                     const int32_t* list, int64_t count, int force, int cap, unsigned char* ws,
                                     size_t ws_bytes, int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list,
-                                    const GKQuery& q, hipStream_t stream) {
+                                    const GKQuery& q, unsigned long long* work, const int32_t* prio,
+                                    const int32_t* prio_count, hipStream_t stream) {
 #define GK_L(V) launch_ingest_t<CAP, V>(st, x, offs, list, count, force, cap, ws, ws_bytes, ws_blocks, \
-                                        ovf_count, ovf_list, q, stream)
+                                        ovf_count, ovf_list, q, work, prio, prio_count, stream)
   switch (vpl) {
     case 1: return GK_L(1);
     case 2: return GK_L(2);
@@ -2172,7 +2276,8 @@ size_t gk_ingest_ws_bytes(int cap, int vpl) { return gk_flush_ws_bytes(cap, vpl)
 hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x, const int64_t* offs,
                             const int32_t* list, int64_t count, int force, unsigned char* ws, size_t ws_bytes,
                             int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list, const GKQuery& q,
-                            unsigned long long* work, hipStream_t stream) {
+                            unsigned long long* work, const int32_t* prio, const int32_t* prio_count,
+                            hipStream_t stream) {
   switch (cap) {
     case SMALL_CAP:
       if (vpl == 1) return launch_ingest_small<1>(st, x, offs, list, count, force, ovf_count, ovf_list, q, work, stream);
@@ -2180,25 +2285,41 @@ hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x
       return hipErrorInvalidValue;
     case 2048:
       return launch_ingest_vpl<2048>(vpl, st, x, offs, list, count, force, cap, nullptr, 0, 0, ovf_count, ovf_list,
-                                     q, stream);
+                                     q, work, prio, prio_count, stream);
     default:
       if (!ws || ws_blocks <= 0) return hipErrorInvalidValue;
       return launch_ingest_vpl<0>(vpl, st, x, offs, list, count, force, cap, ws, ws_bytes, ws_blocks, ovf_count,
-                                  ovf_list, q, stream);
+                                  ovf_list, q, work, prio, prio_count, stream);
   }
 }
 
 hipError_t gk_launch_stats(const GKState& st, const double* x, const int64_t* offs, int32_t* long_list,
-                           int32_t* long_count, hipStream_t stream) {
+                           int64_t* long_n, int32_t* long_count, hipStream_t stream) {
   if (st.S <= 0) return hipSuccess;
   hipError_t e = hipMemsetAsync(long_count, 0, sizeof(int32_t), stream);
   if (e != hipSuccess) return e;
   const int64_t grid = (st.S + 255) / 256;
   hipLaunchKernelGGL(k_stats, dim3((unsigned)grid), dim3(256), 0, stream, st, x, offs, long_list, long_count);
+  hipLaunchKernelGGL(k_long_prep, dim3(1), dim3(1024), 0, stream, st, offs, long_list, long_n,
+                     (const int32_t*)long_count);
+  return hipGetLastError();
+}
+
+hipError_t gk_launch_stats_long(const GKState& st, const double* x, const int64_t* offs, const int32_t* long_list,
+                                const int64_t* long_n, const int32_t* long_count, hipStream_t stream) {
+  if (st.S <= 0) return hipSuccess;
   // the long-stream count is only known on the device: a fixed grid of waves
   // reads it (an empty list costs one short launch)
-  hipLaunchKernelGGL(k_stats_long, dim3((unsigned)(num_cu() * 4)), dim3(64), 0, stream, st, x, offs,
-                     (const int32_t*)long_list, (const int32_t*)long_count);
+  hipLaunchKernelGGL(k_stats_long, dim3((unsigned)(num_cu() * 4)), dim3(64), 0, stream, st, x, offs, long_list,
+                     long_n, long_count);
+  return hipGetLastError();
+}
+
+hipError_t gk_launch_query_list(const GKState& st, const int32_t* list, const int32_t* count, const GKQuery& q,
+                                hipStream_t stream) {
+  if (st.S <= 0 || !q.qs || q.nq <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_query_list, dim3((unsigned)(num_cu() * 4)), dim3(64), 0, stream, st, list, count, q.qs, q.nq,
+                     q.mode, q.out);
   return hipGetLastError();
 }
 

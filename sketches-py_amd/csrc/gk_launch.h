@@ -46,10 +46,21 @@ size_t gk_ingest_ws_bytes(int cap, int vpl);
 hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x, const int64_t* offs,
                             const int32_t* list, int64_t count, int force, unsigned char* ws, size_t ws_bytes,
                             int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list, const GKQuery& q,
-                            unsigned long long* work, hipStream_t stream);
-// long_list (S entries) / long_count: device scratch for the streams handed to k_stats_long
+                            unsigned long long* work, const int32_t* prio, const int32_t* prio_count,
+                            hipStream_t stream);
+// `prio` / `prio_count` (device, may be NULL): streams handed out first by the
+// capacity-class kernels (the long streams of the batch, longest first).
+// k_stats over every stream; streams longer than GK_STATS_LONG values are put
+// on long_list (S entries), sorted longest first, with their pre-call n in
+// long_n, for gk_launch_stats_long, which may run on another HIP stream beside
+// the ingest launches (it writes only _min/_max/_sum/_avg of listed streams).
 hipError_t gk_launch_stats(const GKState& st, const double* x, const int64_t* offs, int32_t* long_list,
-                           int32_t* long_count, hipStream_t stream);
+                           int64_t* long_n, int32_t* long_count, hipStream_t stream);
+hipError_t gk_launch_stats_long(const GKState& st, const double* x, const int64_t* offs, const int32_t* long_list,
+                                const int64_t* long_n, const int32_t* long_count, hipStream_t stream);
+// quantiles of the listed streams from their committed tables (after the join)
+hipError_t gk_launch_query_list(const GKState& st, const int32_t* list, const int32_t* count, const GKQuery& q,
+                                hipStream_t stream);
 size_t gk_merge_lds_bytes(int cap, int pmax);
 hipError_t gk_launch_merge(const MergeArgsHost& h, hipStream_t stream);
 hipError_t gk_launch_reset(const GKState& st, hipStream_t stream);

@@ -398,3 +398,34 @@ def test_long_stream_stats(gpu_device):
             assert_same_state(ss, osx, "long eps=%g part %d" % (eps, part))
         got = ss.quantiles([0.5, 0.9, 0.99]).cpu().numpy()
         assert_same_quantiles(got, osx.quantiles([0.5, 0.9, 0.99]), "long q eps=%g" % eps)
+
+
+def test_fused_query_long_streams_beside_stats(gpu_device):
+    """Long streams (> GK_STATS_LONG values) walk their _sum/_avg chains on a
+    second HIP stream beside the ingest launch, which takes them longest
+    first; the fused query is re-answered for them once _min/_max are final
+    (q = 1.0 returns _max, gk:229).  Lengths are distinct and unordered so the
+    longest-first hand-out differs from stream order."""
+    rng = np.random.default_rng(43)
+    for eps in (0.01, 0.001):
+        S = 48
+        lens = rng.integers(0, 3000, S)
+        lens[rng.choice(S, 9, replace=False)] = [16385, 40000, 17000, 90001, 25000, 60000, 16384, 33000, 70000]
+        dists = rng.integers(0, 8, S)
+        ss = _ss(S, eps, gpu_device)
+        osx = OracleSet(S, eps)
+        for part, (qs, single) in enumerate((([0.0, 0.5, 0.99, 1.0], False), ([1.0, 0.25], False),
+                                             ([0.5, 1.0], True))):
+            seqs = [gen(int(d), int(L) // (part + 1), rng) for d, L in zip(dists, lens)]
+            flat, offs = csr(seqs)
+            got = ss.ingest(torch.from_numpy(flat), torch.from_numpy(offs), quantiles=qs, single=single)
+            osx.ingest(flat, offs)
+            exp = osx.quantiles(qs, single=single)
+            assert_same_quantiles(got.cpu().numpy(), exp, "long fused eps=%g part %d" % (eps, part))
+            assert_same_state(ss, osx, "long fused state eps=%g part %d" % (eps, part))
+        # plain ingest (no query) of long streams, then stats read right away
+        seqs = [gen(int(d), int(L), rng) for d, L in zip(dists, lens)]
+        flat, offs = csr(seqs)
+        ss.ingest(torch.from_numpy(flat), torch.from_numpy(offs))
+        osx.ingest(flat, offs)
+        assert_same_state(ss, osx, "long plain eps=%g" % eps)
