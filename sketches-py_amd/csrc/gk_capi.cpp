@@ -81,6 +81,10 @@ struct gk_set {
   // this stream beside the ingest launches; ev_fork / ev_join order it
   hipStream_t aux = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // presorted flush batches of long streams (sets whose class 0 is the 2048
+  // class): plan arrays, workspace, and the size the last call needed
+  GKPresort ps;
+  int64_t* h_ws_need = nullptr;  // pinned host copy of *ps.ws_need
   // scratch
   double* d_qs = nullptr;
   int qs_alloc = 0;
@@ -221,7 +225,8 @@ hipError_t launch_class(gk_set* h, int c, const double* x, const int64_t* offs, 
                         int force, const GKQuery& q, hipStream_t stream, bool prio = false) {
   return gk_launch_ingest(h->st.cap[c], h->vpl, h->st, x, offs, list, count, force, h->d_ws, h->ws_bytes,
                           h->ws_blocks, h->d_ovf_count, h->d_ovf_list, q, h->d_work,
-                          prio ? h->d_long_list : nullptr, prio ? h->d_long_count : nullptr, stream);
+                          prio ? h->d_long_list : nullptr, prio ? h->d_long_count : nullptr,
+                          prio && h->ps.ws ? h->ps.ws : nullptr, prio && h->ps.ws ? h->ps.list_ws : nullptr, stream);
 }
 
 // gk:52-59 for a batch: k_stats over every stream on `s` (it lists the
@@ -232,17 +237,26 @@ hipError_t launch_class(gk_set* h, int c, const double* x, const int64_t* offs, 
 // their final _min/_max.
 int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s) {
   if (h->timing) HIP_TRY(hipEventRecord(h->ev[2], s));
-  HIP_TRY(gk_launch_stats(h->st, x, offs, h->d_long_list, h->d_long_n, h->d_long_count, s));
-  if (h->timing) HIP_TRY(hipEventRecord(h->ev[3], s));
+  // k_stats + k_long_prep, then the fork (k_stats_long needs only the
+  // sorted list and the pre-call n), then the presort of the long streams'
+  // flush batches on `s`
+  HIP_TRY(gk_launch_stats(h->st, x, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->ps, s));
   HIP_TRY(hipEventRecord(h->ev_fork, s));
   HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_fork, 0));
   HIP_TRY(gk_launch_stats_long(h->st, x, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->aux));
   HIP_TRY(hipEventRecord(h->ev_join, h->aux));
+  HIP_TRY(gk_launch_presort(h->st, x, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->ps, s));
+  if (h->ps.ws_need) HIP_TRY(hipMemcpyAsync(h->h_ws_need, h->ps.ws_need, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  if (h->timing) HIP_TRY(hipEventRecord(h->ev[3], s));
   return GK_OK;
 }
 
+int grow_presort(gk_set* h, hipStream_t s);
+
 int stats_join(gk_set* h, hipStream_t s, const GKQuery& q) {
   HIP_TRY(hipStreamWaitEvent(s, h->ev_join, 0));
+  int rc = grow_presort(h, s);
+  if (rc) return rc;
   HIP_TRY(gk_launch_query_list(h->st, h->d_long_list, h->d_long_count, q, s));
   if (h->timing) {
     float ms = 0;
@@ -255,6 +269,27 @@ int stats_join(gk_set* h, hipStream_t s, const GKQuery& q) {
 // Launch the ingest/flush kernel over every stream (class 0 over all, each
 // larger class over its member list); streams that overflow their class were
 // not committed, so they are promoted one class up and run again.
+// The presort workspace is sized from what the previous call needed (read
+// back after the call; a call whose batches do not fit runs those streams
+// unsorted -- same results, slower flushes).
+int grow_presort(gk_set* h, hipStream_t s) {
+  if (!h->ps.ws_need) return GK_OK;
+  HIP_TRY(hipStreamSynchronize(s));  // the ingest launches synchronise anyway
+  const int64_t need = *h->h_ws_need;
+  if (need <= h->ps.ws_cap) return GK_OK;
+  const int64_t cap = std::max<int64_t>(need + need / 8, 1 << 20);
+  if (h->ps.ws) (void)hipFree(h->ps.ws);
+  h->ps.ws = nullptr;
+  h->ps.ws_cap = 0;
+  if (hipMalloc(&h->ps.ws, (size_t)cap * sizeof(double)) != hipSuccess) {
+    h->ps.ws = nullptr;  // not fatal: long streams flush unsorted
+    (void)hipGetLastError();
+    return GK_OK;
+  }
+  h->ps.ws_cap = cap;
+  return GK_OK;
+}
+
 int run_ingest(gk_set* h, const double* x, const int64_t* offs, int force, hipStream_t stream,
                const GKQuery& q = GKQuery(), bool prio = false) {
   if (!offs) offs = h->d_zero_offs;
@@ -425,6 +460,13 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
   okm &= hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking) == hipSuccess;
   okm &= hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) == hipSuccess;
   okm &= hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) == hipSuccess;
+  if (h->P > 128) {  // class 0 is a capacity-class kernel: presort long streams' batches
+    okm &= hipMalloc(&h->ps.list_ws, S * sizeof(int64_t)) == hipSuccess;
+    okm &= hipMalloc(&h->ps.list_b0, (S + 1) * sizeof(int64_t)) == hipSuccess;
+    okm &= hipMalloc(&h->ps.ws_need, sizeof(int64_t)) == hipSuccess;
+    okm &= hipHostMalloc(&h->h_ws_need, sizeof(int64_t)) == hipSuccess;
+    if (h->h_ws_need) *h->h_ws_need = 0;
+  }
   if (!okm) {
     gk_destroy(h);
     return fail(GK_E_NOMEM, "device allocation for %lld streams failed", (long long)num_streams);
@@ -454,7 +496,8 @@ int gk_destroy(gk_set* h) {
                   st.avg,     st.cls,         st.slot,          st.tab[0],      st.tab[1],     st.tab[2],
                   st.pbuf,    h->d_list[0],   h->d_list[1],     h->d_list[2],   h->d_qs,       h->d_ovf_count,
                   h->d_ovf_list, h->d_tmp_list, h->d_tmp_slots, h->d_ws, h->d_zero_offs, h->d_work,
-                  h->d_long_list, h->d_long_n, h->d_long_count};
+                  h->d_long_list, h->d_long_n, h->d_long_count, h->ps.list_ws, h->ps.list_b0, h->ps.ws,
+                  h->ps.ws_need};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (auto& e : h->ev)
@@ -462,6 +505,7 @@ int gk_destroy(gk_set* h) {
   if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
   if (h->ev_join) (void)hipEventDestroy(h->ev_join);
   if (h->aux) (void)hipStreamDestroy(h->aux);
+  if (h->h_ws_need) (void)hipHostFree(h->h_ws_need);
   delete h;
   return GK_OK;
 }

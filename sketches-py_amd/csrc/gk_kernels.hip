@@ -23,6 +23,45 @@
 #include "gk_state.h"
 #include "gk_launch.h"
 
+#define GK_PROF_NSEC 12
+#ifdef GK_PROF
+__device__ unsigned long long gk_prof_acc[GK_PROF_NSEC];
+__device__ __forceinline__ uint32_t gk_cycles() { return (uint32_t)__builtin_amdgcn_s_memtime(); }
+#define GK_MARK(L, sec)                                      \
+  do {                                                       \
+    if (threadIdx.x == 0) {                                  \
+      const uint32_t t_ = gk_cycles();                       \
+      (L).prof[sec] += (uint32_t)(t_ - (L).prof_t);         \
+      (L).prof_t = t_;                                       \
+    }                                                        \
+  } while (0)
+#else
+#define GK_MARK(L, sec) do { } while (0)
+#endif
+// capacity-class kernels (k_ingest<CAP>): one LDS accumulator set per block,
+// marked by lane 0 (GK_BMARK), summed into gk_prof_acc at the end
+#ifdef GK_PROF
+struct GKBigProf {
+  unsigned long long acc[GK_PROF_NSEC];
+  uint32_t t;
+};
+__device__ __forceinline__ GKBigProf& gk_big_prof() {
+  __shared__ GKBigProf p;
+  return p;
+}
+#define GK_BMARK(sec)                                        \
+  do {                                                       \
+    if (threadIdx.x == 0) {                                  \
+      GKBigProf& p_ = gk_big_prof();                         \
+      const uint32_t t_ = gk_cycles();                       \
+      p_.acc[sec] += (uint32_t)(t_ - p_.t);                  \
+      p_.t = t_;                                             \
+    }                                                        \
+  } while (0)
+#else
+#define GK_BMARK(sec) do { } while (0)
+#endif
+
 #define GK_KEEP_BIT 0x40000000
 
 // Largest T handled with int32 arithmetic: T = floor(2 eps (n-1)) is clamped
@@ -298,7 +337,9 @@ __global__ __launch_bounds__(256) void k_stats(GKState st, const double* __restr
 
 __global__ __launch_bounds__(1024) void k_long_prep(GKState st, const int64_t* __restrict__ offs,
                                                     int32_t* __restrict__ list, int64_t* __restrict__ list_n,
-                                                    const int32_t* __restrict__ count) {
+                                                    const int32_t* __restrict__ count,
+                                                    int64_t* __restrict__ list_ws, int64_t* __restrict__ list_b0,
+                                                    int64_t ws_cap, int64_t* __restrict__ ws_need) {
   __shared__ uint64_t key[GK_SORT_LONG_MAX];
   const int cnt = *count;
   const int t = threadIdx.x;
@@ -336,6 +377,123 @@ __global__ __launch_bounds__(1024) void k_long_prep(GKState st, const int64_t* _
     __syncthreads();
   }
   for (int i = t; i < cnt; i += 1024) list_n[i] = st.n[list[i]];
+  if (!list_ws) return;
+  __syncthreads();
+  // Presort plan (k_presort): every automatic flush of a listed class-0
+  // stream in this call gets a slot of P doubles in the workspace; list_ws[i]
+  // = first slot offset (in doubles) or -1 (not presorted: the workspace is
+  // too small -- the host grows it from *ws_need after the call), list_b0[i]
+  // = the stream's first global batch index (for k_presort's block mapping).
+  __shared__ int64_t part[1024];
+  const int per = (cnt + 1023) / 1024;
+  const int i0 = t * per, i1 = min(i0 + per, cnt);
+  int64_t mine = 0;
+  for (int i = i0; i < i1; ++i) {
+    const int64_t s = list[i];
+    int64_t nb = 0;
+    if (st.cls[s] == 0) {
+      const int64_t L = offs[s + 1] - offs[s];
+      const int64_t need = st.P - (list_n[i] % st.P);
+      nb = L >= need ? 1 + (L - need) / st.P : 0;
+    }
+    list_b0[i] = nb;  // count for now
+    mine += nb;
+  }
+  part[t] = mine;
+  __syncthreads();
+  if (t == 0) {
+    int64_t acc = 0;
+    for (int k = 0; k < 1024; ++k) {
+      const int64_t v = part[k];
+      part[k] = acc;
+      acc += v;
+    }
+    *ws_need = acc * st.P;
+    list_b0[cnt] = acc;  // total batches (k_presort's grid bound)
+  }
+  __syncthreads();
+  int64_t b = part[t];
+  for (int i = i0; i < i1; ++i) {
+    const int64_t nb = list_b0[i];
+    list_b0[i] = b;
+    list_ws[i] = (nb > 0 && (b + nb) * st.P <= ws_cap) ? b * st.P : -1;
+    b += nb;
+  }
+}
+
+// ===========================================================================
+// k_presort: the batch of every automatic flush of a listed long stream
+// (list_ws >= 0), sorted by (value, insertion index) -- Python's stable
+// sorted() of gk:71-72 -- into its workspace slot, ahead of k_ingest, so that
+// the flush (sequential per stream, on the critical path of long streams)
+// skips its in-gap ranking.  Batch 0 is the pre-call pending values followed
+// by the first `need` values; batch b > 0 is the next P values.  One
+// 256-thread block per batch (global batch id -> stream by binary search over
+// list_b0), bitonic sort of up to 1024 keys in LDS.
+// ===========================================================================
+__global__ __launch_bounds__(256) void k_presort(GKState st, const double* __restrict__ x,
+                                                 const int64_t* __restrict__ offs,
+                                                 const int32_t* __restrict__ list, const int32_t* __restrict__ count,
+                                                 const int64_t* __restrict__ list_n,
+                                                 const int64_t* __restrict__ list_ws,
+                                                 const int64_t* __restrict__ list_b0, double* __restrict__ ws) {
+  __shared__ double kv[1024];
+  __shared__ uint32_t ki[1024];
+  const int cnt = *count;
+  if (cnt <= 0) return;
+  const int64_t total = list_b0[cnt];
+  const int t = threadIdx.x;
+  const int P = st.P;
+  for (int64_t gb = blockIdx.x; gb < total; gb += gridDim.x) {
+    // stream slot i: the last list_b0[i] <= gb
+    int lo = 0, hi = cnt - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (list_b0[mid] <= gb) lo = mid;
+      else hi = mid - 1;
+    }
+    const int i = lo;
+    const int64_t wso = list_ws[i];
+    if (wso < 0) continue;  // block-uniform
+    const int64_t b = gb - list_b0[i];
+    const int64_t s = list[i];
+    const int64_t xo = offs[s];
+    const int p = st.pend[s];
+    const int64_t need = P - (list_n[i] % P);
+    const double* pb = st.pbuf + s * (int64_t)st.pmax;
+    const int m = b == 0 ? p + (int)need : P;
+    const int64_t xb = b == 0 ? xo : xo + need + (b - 1) * P;  // first x value of the batch (after pending)
+    int N = 64;
+    while (N < m) N <<= 1;
+    for (int k = t; k < N; k += 256) {
+      double v = __longlong_as_double(0x7ff0000000000000LL);
+      if (k < m) v = (b == 0 && k < p) ? pb[k] : x[xb + (b == 0 ? k - p : k)];
+      kv[k] = v;
+      ki[k] = k < m ? (uint32_t)k : 0xffffffffu;
+    }
+    __syncthreads();
+    for (int k = 2; k <= N; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int pp = t; pp < N / 2; pp += 256) {
+          const int a = ((pp & ~(j - 1)) << 1) | (pp & (j - 1));
+          const int c = a + j;
+          const double va = kv[a], vc = kv[c];
+          const uint32_t ia = ki[a], ic = ki[c];
+          const bool a_gt = (va > vc) || (!(va < vc) && ia > ic);
+          if (a_gt == ((a & k) == 0)) {
+            kv[a] = vc;
+            kv[c] = va;
+            ki[a] = ic;
+            ki[c] = ia;
+          }
+        }
+        __syncthreads();
+      }
+    }
+    double* out = ws + wso + b * P;
+    for (int k = t; k < m; k += 256) out[k] = kv[k];
+    __syncthreads();
+  }
 }
 
 // ===========================================================================
@@ -387,9 +545,20 @@ __global__ __launch_bounds__(64) void k_stats_long(GKState st, const double* __r
           q[d] = (nx < L) ? x[xo + nx] : 0.0;
           wsync<false>();
           if (cn == 64) {
-#pragma unroll 8
+            // the chain is latency-bound: keep GK_SL_AHEAD broadcast reads in
+            // flight (a ring of registers refilled as each entry is consumed;
+            // sched_barrier pins each refill before the chain step it hides)
+#ifndef GK_SL_AHEAD
+#define GK_SL_AHEAD 12
+#endif
+            double2 ring[GK_SL_AHEAD];
+#pragma unroll
+            for (int k = 0; k < GK_SL_AHEAD; ++k) ring[k] = buf[k];
+#pragma unroll
             for (int j = 0; j < 64; ++j) {
-              const double2 e = buf[j];
+              const double2 e = ring[j % GK_SL_AHEAD];
+              if (j + GK_SL_AHEAD < 64) ring[j % GK_SL_AHEAD] = buf[j + GK_SL_AHEAD];
+              __builtin_amdgcn_sched_barrier(0);
               sm = sm + e.x;                    // gk:53
               av = av + (e.x - av) * e.y;       // gk:54
             }
@@ -568,7 +737,7 @@ __device__ __forceinline__ void emit_value(const FlushBuf& L, double* nv, int32_
 template <int VPL, bool GLOBAL, typename AfterSearch>
 __device__ __forceinline__ int flush_wave(const FlushBuf& L, const int cap, const int cur, const int E,
                                           const double (&xv)[VPL], const int cnt, const int T,
-                                          const int lane, AfterSearch&& after_search) {
+                                          const int lane, AfterSearch&& after_search, const bool presorted) {
   // selects, not L.tv[cur]: a runtime index into the pointer pair would put
   // the pair in scratch memory
   const double* __restrict__ tv = cur ? L.tv[1] : L.tv[0];
@@ -596,6 +765,7 @@ __device__ __forceinline__ int flush_wave(const FlushBuf& L, const int cap, cons
   }
 #pragma unroll
   for (int r = 0; r < VPL; ++r) xg[r] = min(xg[r], E);
+  GK_BMARK(1);
   after_search();
   for (int j = lane; j <= E; j += 64) L.gpk[j] = 0u;
   wsync<GLOBAL>();
@@ -609,7 +779,8 @@ __device__ __forceinline__ int flush_wave(const FlushBuf& L, const int cap, cons
   uint32_t mloc = 0;
 #pragma unroll
   for (int r = 0; r < VPL; ++r) mloc = max(mloc, xs[r] + 1u);
-  const bool use_sort = wave_max_u32(mloc) > GK_RANK_LOOP_MAX;
+  const bool use_sort = !presorted && wave_max_u32(mloc) > GK_RANK_LOOP_MAX;
+  GK_BMARK(2);
 
   // ---- carry walk over the entries (closed form of gk:93-106) --------------
   // Lane l owns the contiguous block [l*K, l*K+K).  A lane can run its block
@@ -658,6 +829,7 @@ __device__ __forceinline__ int flush_wave(const FlushBuf& L, const int cap, cons
       }
       if (__all(done)) break;
     }
+    GK_BMARK(3);
     uint32_t sm = 0, so = 0;
     for (int j = j0; j < jend; ++j) {
       const int m = (int)L.gpk[j];
@@ -695,9 +867,19 @@ __device__ __forceinline__ int flush_wave(const FlushBuf& L, const int cap, cons
   }
   const int totm = (int)(total >> 16);
   wsync<GLOBAL>();
+  GK_BMARK(4);
 
   // ---- stable order inside each gap (gk:72), then emit --------------------
-  if (!use_sort) {
+  if (presorted) {
+    // values arrive in (value, insertion index) order (k_presort): the rank
+    // inside the gap is the position minus the gap's base
+#pragma unroll
+    for (int r = 0; r < VPL; ++r) {
+      const int q = lane + 64 * r;
+      if (q < cnt) emit_value(L, nv, ng, nd, E, totm, cs, xv[r], xg[r], q - (int)(L.gpk[xg[r]] >> 16));
+    }
+    GK_BMARK(5);
+  } else if (!use_sort) {
     // small gaps: scatter by gap, rank by comparison with the gap's members
 #pragma unroll
     for (int r = 0; r < VPL; ++r) {
@@ -732,6 +914,7 @@ __device__ __forceinline__ int flush_wave(const FlushBuf& L, const int cap, cons
         emit_value(L, nv, ng, nd, E, totm, cs, x, gap, rk);
       }
     }
+    GK_BMARK(5);
   } else {
     // a large gap (first flush: everything is tail; adversarial orders):
     // bitonic sort of all values by (value, insertion index); all values of
@@ -773,9 +956,11 @@ __device__ __forceinline__ int flush_wave(const FlushBuf& L, const int cap, cons
         emit_value(L, nv, ng, nd, E, totm, cs, x, gap, rk);
       }
     }
+    GK_BMARK(6);
   }
   gk_pad_table(nv, newE, lane);
   wsync<GLOBAL>();
+  GK_BMARK(7);
   return newE;
 }
 
@@ -916,7 +1101,9 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
                                                int nq, double* __restrict__ qout, int qmode,
                                                unsigned long long* __restrict__ work,
                                                const int32_t* __restrict__ prio,
-                                               const int32_t* __restrict__ prio_count) {
+                                               const int32_t* __restrict__ prio_count,
+                                               const double* __restrict__ psort,
+                                               const int64_t* __restrict__ prio_ws) {
   constexpr int LCAP = CAP > 0 ? CAP : 1;
   constexpr int LVPL = CAP > 0 ? VPL : 1;
   __shared__ FlushLDS<LCAP, LVPL> Ls;
@@ -929,6 +1116,12 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
   }
   const int lane = threadIdx.x;
   const int P = st.P;
+#ifdef GK_PROF
+  if (lane == 0) {
+    for (int i = 0; i < GK_PROF_NSEC; ++i) gk_big_prof().acc[i] = 0;
+    gk_big_prof().t = gk_cycles();
+  }
+#endif
   // headers are prefetched one stream ahead; flush-only launches pass
   // x == NULL and an all-zero offs array
   // Streams are handed out dynamically (one atomic per stream on `work`,
@@ -953,6 +1146,8 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
   for (; w < total;) {
     const int64_t s = sid(w);
     const bool from_prio = w < npri;
+    // presorted automatic-flush batches of this stream (k_presort), or none
+    const int64_t wso = (from_prio && prio_ws) ? rfl64(prio_ws[w]) : -1;
     const int64_t wn = grab();
     const int32_t scls = __builtin_amdgcn_readfirstlane(hv.cls);
     const int32_t sslot = __builtin_amdgcn_readfirstlane(hv.slot);
@@ -997,6 +1192,7 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
     }
     if (E <= cap - 1) gk_pad_table(B.tv[0], E, lane);
     wsync<CAP == 0>();
+    GK_BMARK(0);
 
     // an imported / merged table with no room for the search padding goes
     // straight to the overflow path (promotion)
@@ -1008,23 +1204,36 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
     // loaded one flush ahead: their HBM latency hides under the current
     // flush's LDS work.
     double xv[VPL];
-    if (ok && used + need <= Lx) gk_load_flush_values<VPL>(xv, pb, p, x + xo, p + (int)need, lane);
+    // presorted batch b lives at psort + wso + b*P (k_presort, same values)
+    const double* __restrict__ sb = wso >= 0 ? psort + wso : nullptr;
+    if (ok && used + need <= Lx) {
+      if (sb) {
+#pragma unroll
+        for (int r = 0; r < VPL; ++r) xv[r] = sb[min(lane + 64 * r, p + (int)need - 1)];
+      } else {
+        gk_load_flush_values<VPL>(xv, pb, p, x + xo, p + (int)need, lane);
+      }
+    }
     while (ok && used + need <= Lx) {
       const int cnt = p + (int)need;
       const int64_t nused = used + need;
       const int navail = (int)min((int64_t)P, Lx - nused);  // next flush, or the leftover tail
+      const bool cur_sorted = sb != nullptr;
       double xn[VPL];
 #pragma unroll
       for (int r = 0; r < VPL; ++r) xn[r] = 0.0;
       auto prefetch = [&]() {
         if (navail > 0) {
-          const double* base = x + xo + nused;
+          // a full next batch comes presorted; the leftover tail does not
+          const double* base = (sb && navail == P) ? sb + P : x + xo + nused;
 #pragma unroll
           for (int r = 0; r < VPL; ++r) xn[r] = base[min(lane + 64 * r, navail - 1)];
         }
       };
       n += need;
-      const int nE = flush_wave<VPL, CAP == 0>(B, cap, cur, E, xv, cnt, gk_threshold(st, n), lane, prefetch);
+      GK_BMARK(8);
+      const int nE = flush_wave<VPL, CAP == 0>(B, cap, cur, E, xv, cnt, gk_threshold(st, n), lane, prefetch,
+                                               cur_sorted);
       if (nE < 0) {
         ok = false;
         break;
@@ -1035,6 +1244,7 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
       p = 0;
       need = P;
       flushed = true;
+      if (sb) sb = navail == P ? sb + P : nullptr;
 #pragma unroll
       for (int r = 0; r < VPL; ++r) xv[r] = (lane + 64 * r < navail) ? xn[r] : 0.0;
     }
@@ -1045,7 +1255,7 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
         const int cnt = p + (int)rem;
         if (!flushed) gk_load_flush_values<VPL>(xv, pb, p, x ? x + xo + used : pb, cnt, lane);
         n += rem;
-        const int nE = flush_wave<VPL, CAP == 0>(B, cap, cur, E, xv, cnt, gk_threshold(st, n), lane, [] {});
+        const int nE = flush_wave<VPL, CAP == 0>(B, cap, cur, E, xv, cnt, gk_threshold(st, n), lane, [] {}, false);
         if (nE < 0) {
           ok = false;
         } else {
@@ -1094,7 +1304,12 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
       st.pend[s] = p;
     }
     wsync<CAP == 0>();
+    GK_BMARK(9);
   }
+#ifdef GK_PROF
+  if (lane == 0)
+    for (int i = 0; i < GK_PROF_NSEC; ++i) atomicAdd(&gk_prof_acc[i], gk_big_prof().acc[i]);
+#endif
 }
 
 // ===========================================================================
@@ -1135,21 +1350,6 @@ __device__ __forceinline__ int pidx(int i) { return i + (i >> 5); }
 // Section profiler (profiling builds only, -DGK_PROF; tools/prof_sections.py):
 // lane 0 adds the s_memtime delta since the previous mark to a per-block
 // LDS counter; the block adds its counters to gk_prof_acc when it ends.
-#define GK_PROF_NSEC 12
-#ifdef GK_PROF
-__device__ unsigned long long gk_prof_acc[GK_PROF_NSEC];
-__device__ __forceinline__ uint32_t gk_cycles() { return (uint32_t)__builtin_amdgcn_s_memtime(); }
-#define GK_MARK(L, sec)                                      \
-  do {                                                       \
-    if (threadIdx.x == 0) {                                  \
-      const uint32_t t_ = gk_cycles();                       \
-      (L).prof[sec] += (uint32_t)(t_ - (L).prof_t);         \
-      (L).prof_t = t_;                                       \
-    }                                                        \
-  } while (0)
-#else
-#define GK_MARK(L, sec) do { } while (0)
-#endif
 
 template <int VPL>
 struct SmallLDS {
@@ -2209,7 +2409,7 @@ static hipError_t launch_ingest_t(const GKState& st, const double* x, const int6
                                   unsigned char* ws, size_t ws_bytes, int64_t ws_blocks,
                                   int32_t* ovf_count, int32_t* ovf_list, const GKQuery& q,
                                   unsigned long long* work, const int32_t* prio, const int32_t* prio_count,
-                                  hipStream_t stream) {
+                                  const double* psort, const int64_t* prio_ws, hipStream_t stream) {
   if (count <= 0) return hipSuccess;
   if (!work) return hipErrorInvalidValue;
   int64_t grid;
@@ -2228,7 +2428,7 @@ static hipError_t launch_ingest_t(const GKState& st, const double* x, const int6
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((k_ingest<CAP, VPL>), dim3((unsigned)grid), dim3(64), 0, stream, st, x, offs, list,
                      count, force, cap, ws, ws_bytes, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode, work,
-                     prio, prio_count);
+                     prio, prio_count, psort, prio_ws);
   return hipGetLastError();
 }
 
@@ -2237,9 +2437,10 @@ static hipError_t launch_ingest_vpl(int vpl, const GKState& st, const double* x,
                                     const int32_t* list, int64_t count, int force, int cap, unsigned char* ws,
                                     size_t ws_bytes, int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list,
                                     const GKQuery& q, unsigned long long* work, const int32_t* prio,
-                                    const int32_t* prio_count, hipStream_t stream) {
+                                    const int32_t* prio_count, const double* psort, const int64_t* prio_ws,
+                                    hipStream_t stream) {
 #define GK_L(V) launch_ingest_t<CAP, V>(st, x, offs, list, count, force, cap, ws, ws_bytes, ws_blocks, \
-                                        ovf_count, ovf_list, q, work, prio, prio_count, stream)
+                                        ovf_count, ovf_list, q, work, prio, prio_count, psort, prio_ws, stream)
   switch (vpl) {
     case 1: return GK_L(1);
     case 2: return GK_L(2);
@@ -2277,7 +2478,7 @@ hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x
                             const int32_t* list, int64_t count, int force, unsigned char* ws, size_t ws_bytes,
                             int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list, const GKQuery& q,
                             unsigned long long* work, const int32_t* prio, const int32_t* prio_count,
-                            hipStream_t stream) {
+                            const double* psort, const int64_t* prio_ws, hipStream_t stream) {
   switch (cap) {
     case SMALL_CAP:
       if (vpl == 1) return launch_ingest_small<1>(st, x, offs, list, count, force, ovf_count, ovf_list, q, work, stream);
@@ -2285,23 +2486,32 @@ hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x
       return hipErrorInvalidValue;
     case 2048:
       return launch_ingest_vpl<2048>(vpl, st, x, offs, list, count, force, cap, nullptr, 0, 0, ovf_count, ovf_list,
-                                     q, work, prio, prio_count, stream);
+                                     q, work, prio, prio_count, psort, prio_ws, stream);
     default:
       if (!ws || ws_blocks <= 0) return hipErrorInvalidValue;
       return launch_ingest_vpl<0>(vpl, st, x, offs, list, count, force, cap, ws, ws_bytes, ws_blocks, ovf_count,
-                                  ovf_list, q, work, prio, prio_count, stream);
+                                  ovf_list, q, work, prio, prio_count, psort, prio_ws, stream);
   }
 }
 
 hipError_t gk_launch_stats(const GKState& st, const double* x, const int64_t* offs, int32_t* long_list,
-                           int64_t* long_n, int32_t* long_count, hipStream_t stream) {
+                           int64_t* long_n, int32_t* long_count, const GKPresort& ps, hipStream_t stream) {
   if (st.S <= 0) return hipSuccess;
   hipError_t e = hipMemsetAsync(long_count, 0, sizeof(int32_t), stream);
   if (e != hipSuccess) return e;
   const int64_t grid = (st.S + 255) / 256;
   hipLaunchKernelGGL(k_stats, dim3((unsigned)grid), dim3(256), 0, stream, st, x, offs, long_list, long_count);
   hipLaunchKernelGGL(k_long_prep, dim3(1), dim3(1024), 0, stream, st, offs, long_list, long_n,
-                     (const int32_t*)long_count);
+                     (const int32_t*)long_count, ps.list_ws, ps.list_b0, ps.ws_cap, ps.ws_need);
+  return hipGetLastError();
+}
+
+hipError_t gk_launch_presort(const GKState& st, const double* x, const int64_t* offs, const int32_t* long_list,
+                             const int64_t* long_n, const int32_t* long_count, const GKPresort& ps,
+                             hipStream_t stream) {
+  if (st.S <= 0 || !ps.list_ws || !ps.ws || ps.ws_cap <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_presort, dim3((unsigned)(num_cu() * 8)), dim3(256), 0, stream, st, x, offs, long_list,
+                     long_count, long_n, (const int64_t*)ps.list_ws, (const int64_t*)ps.list_b0, ps.ws);
   return hipGetLastError();
 }
 

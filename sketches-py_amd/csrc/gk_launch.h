@@ -47,15 +47,31 @@ hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x
                             const int32_t* list, int64_t count, int force, unsigned char* ws, size_t ws_bytes,
                             int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list, const GKQuery& q,
                             unsigned long long* work, const int32_t* prio, const int32_t* prio_count,
-                            hipStream_t stream);
+                            const double* psort, const int64_t* prio_ws, hipStream_t stream);
 // `prio` / `prio_count` (device, may be NULL): streams handed out first by the
-// capacity-class kernels (the long streams of the batch, longest first).
+// capacity-class kernels (the long streams of the batch, longest first);
+// `psort` / `prio_ws`: their presorted flush batches (GKPresort), or NULL.
 // k_stats over every stream; streams longer than GK_STATS_LONG values are put
 // on long_list (S entries), sorted longest first, with their pre-call n in
 // long_n, for gk_launch_stats_long, which may run on another HIP stream beside
 // the ingest launches (it writes only _min/_max/_sum/_avg of listed streams).
+// Presort of the long streams' automatic-flush batches (sets whose class 0 is
+// a capacity-class kernel): per list slot the workspace offset (-1: none)
+// and first global batch, the workspace (ws_cap doubles) and the size this
+// call needed (host grows the workspace from it after the call).
+struct GKPresort {
+  int64_t* list_ws = nullptr;  // [S]
+  int64_t* list_b0 = nullptr;  // [S + 1]
+  double* ws = nullptr;
+  int64_t ws_cap = 0;
+  int64_t* ws_need = nullptr;  // device, 1 value
+};
 hipError_t gk_launch_stats(const GKState& st, const double* x, const int64_t* offs, int32_t* long_list,
-                           int64_t* long_n, int32_t* long_count, hipStream_t stream);
+                           int64_t* long_n, int32_t* long_count, const GKPresort& ps, hipStream_t stream);
+// k_presort over the plan k_long_prep wrote (no-op without a workspace)
+hipError_t gk_launch_presort(const GKState& st, const double* x, const int64_t* offs, const int32_t* long_list,
+                             const int64_t* long_n, const int32_t* long_count, const GKPresort& ps,
+                             hipStream_t stream);
 hipError_t gk_launch_stats_long(const GKState& st, const double* x, const int64_t* offs, const int32_t* long_list,
                                 const int64_t* long_n, const int32_t* long_count, hipStream_t stream);
 // quantiles of the listed streams from their committed tables (after the join)

@@ -24,19 +24,30 @@ SECTIONS = ["stream setup (header, table load)", "gap search", "counts (zero, at
             "entries + carry + scan", "keeps + per-gap info", "rank loop + emit", "bitonic sort + emit",
             "pad + end of flush", "between flushes (values, T)", "leftover, quantiles, write-back", "-", "-"]
 
+SECTIONS_BIG = ["stream setup (header, table load)", "gap search", "counts (zero, atomics, max gap)",
+                "carry walk (rounds)", "sums + scan + keeps", "rank loop + emit", "bitonic sort + emit",
+                "pad + end of flush", "between flushes", "leftover, quantiles, write-back", "-", "-"]
+
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", default="cfg3", choices=["cfg3", "cfg2"])
+    ap.add_argument("--workload", default="cfg3", choices=["cfg3", "cfg2", "long"])
     ap.add_argument("--streams", type=int, default=0)
     a = ap.parse_args()
     from bench import make_input
     from gkarray_amd import StreamSet
-    S, L, dist_name = {"cfg3": (1_000_000, 1000, "pareto"), "cfg2": (100_000, 10_000, "lognormal")}[a.workload]
+    S, L, dist_name = {"cfg3": (1_000_000, 1000, "pareto"), "cfg2": (100_000, 10_000, "lognormal"),
+                       "long": (64, 1_000_000, "lognormal")}[a.workload]
     S = a.streams or S
     dev = torch.device("cuda", 0)
     x, offs = make_input(S, L, 3, dev, dist_name)
-    ss = StreamSet(S, 0.01, device=dev)
+    # "long": eps=0.001 streams of 1M values in the 2048 class (k_ingest<2048>,
+    # sections of flush_wave: SECTIONS_BIG)
+    eps = 0.001 if a.workload == "long" else 0.01
+    global SECTIONS
+    if a.workload == "long":
+        SECTIONS = SECTIONS_BIG
+    ss = StreamSet(S, eps, device=dev)
     lib = ctypes.CDLL(os.environ["GK_LIB_PATH"])
     acc = (ctypes.c_ulonglong * 12)()
     for it in range(2):
