@@ -8,19 +8,23 @@ Two ways streams meet several GPUs:
 * **row-sharded** -- every rank sketched a slice of the rows of the SAME
   streams; the sketches are combined with the reference's left fold
   ``sk_0.merge(sk_1) ... .merge(sk_{N-1})`` (gk:111-154).  ``merge_row_shards``
-  all-gathers the per-rank states (sizes first, then padded payloads) and each
-  rank folds, in rank order, the streams of its own range -- the merge work is
-  split N ways and the result is stream-sharded.
+  hands every rank the N shard states of the streams of its own range and the
+  rank folds them in rank order -- the merge work is split N ways and the
+  result is stream-sharded.  The default exchange is an all-to-all
+  (``alltoall_states``: rank r sends each peer only that peer's stream range,
+  so every table crosses xGMI once); ``exchange="allgather"`` moves every
+  rank's whole state to every rank (N-1 times the bytes).
 
 The exchange helpers (``pack_state`` / ``unpack_state`` / ``all_gather_varlen``
-/ ``allgather_states`` / ``slice_state``) work on tensors of any device, so the
+/ ``allgather_states`` / ``alltoall_states`` / ``slice_state``) work on tensors of any device, so the
 same code runs over gloo on CPU tensors.
 """
 import torch
 import torch.distributed as dist
 
 __all__ = ["stream_range", "balanced_assignment", "pack_state", "unpack_state", "all_gather_varlen",
-           "allgather_states", "slice_state", "concat_states", "fold_states", "merge_row_shards"]
+           "allgather_states", "alltoall_states", "slice_state", "concat_states", "fold_states",
+           "merge_row_shards"]
 
 _F64 = ("v", "pv", "min", "max", "sum", "avg")
 _I64 = ("offs", "poffs", "n")
@@ -95,6 +99,35 @@ def allgather_states(state, group=None):
             for a, b, c, l in zip(fs, is_, js, lt)]
 
 
+def alltoall_states(state, group=None):
+    """Row-shard exchange by all-to-all: this rank's state is cut into the
+    ``stream_range`` of every rank and part r goes to rank r only.  Returns
+    the list (indexed by source rank) of the states of THIS rank's stream
+    range.  One all-to-all of counts (fixed size), then one variable-size
+    ``all_to_all_single`` per payload dtype."""
+    world = dist.get_world_size(group)
+    S = int(state["n"].numel())
+    dev = state["n"].device
+    parts = [pack_state(slice_state(state, *stream_range(S, world, r))) for r in range(world)]
+    nlen = len(_F64 + _I64 + _I32)
+    # per destination: payload lengths (f, i, j) and the component lengths
+    meta = torch.tensor([[p[0].numel(), p[1].numel(), p[2].numel()] + p[3] for p in parts],
+                        dtype=torch.int64, device=dev)
+    flat_in = meta.reshape(-1).contiguous()
+    flat_out = torch.empty_like(flat_in)
+    dist.all_to_all_single(flat_out, flat_in, group=group)
+    rmeta = flat_out.reshape(world, 3 + nlen).cpu()
+    out = []
+    for k in range(3):
+        src = torch.cat([p[k] for p in parts])
+        recv = torch.empty(int(rmeta[:, k].sum()), dtype=src.dtype, device=dev)
+        dist.all_to_all_single(recv, src, output_split_sizes=rmeta[:, k].tolist(),
+                               input_split_sizes=[int(p[k].numel()) for p in parts], group=group)
+        out.append(list(torch.split(recv, rmeta[:, k].tolist())))
+    return [unpack_state(out[0][r], out[1][r], out[2][r], [int(x) for x in rmeta[r, 3:].tolist()], state["eps"])
+            for r in range(world)]
+
+
 def slice_state(state, a, b):
     """The state of streams [a, b) of a CSR state dict."""
     offs, poffs = state["offs"], state["poffs"]
@@ -140,19 +173,26 @@ def fold_states(states, device=None):
     return acc
 
 
-def merge_row_shards(ss, group=None):
+def merge_row_shards(ss, group=None, exchange="alltoall"):
     """Row-sharded sketches -> merged sketches of this rank's stream range.
 
     `ss` is this rank's StreamSet over all S streams (built from its slice of
     the rows).  Returns (StreamSet over streams [a, b), (a, b)); the fold is in
     rank order, identical to the reference's sk0.merge(sk1)...merge(skN-1).
+    `exchange`: "alltoall" (each table crosses once) or "allgather".
     """
+    if exchange not in ("alltoall", "allgather"):
+        raise ValueError("exchange must be 'alltoall' or 'allgather'")
     if not (dist.is_available() and dist.is_initialized()):
         states, world, rank = [ss.export_state()], 1, 0
+        a, b = stream_range(ss.num_streams, world, rank)
+        mine = [slice_state(st, a, b) for st in states]
     else:
         world = dist.get_world_size(group)
         rank = dist.get_rank(group)
-        states = allgather_states(ss.export_state(), group)
-    a, b = stream_range(ss.num_streams, world, rank)
-    mine = [slice_state(st, a, b) for st in states]
+        a, b = stream_range(ss.num_streams, world, rank)
+        if exchange == "alltoall":
+            mine = alltoall_states(ss.export_state(), group)
+        else:
+            mine = [slice_state(st, a, b) for st in allgather_states(ss.export_state(), group)]
     return fold_states(mine, device=ss.device), (a, b)

@@ -89,6 +89,10 @@ def _worker(rank, world, port, S, eps, q):
         ok_exchange = all(same_state(states[r], oracle_state(*shard_data(r, S, eps), S, eps))
                           for r in range(world))
         a, b = gd.stream_range(S, world, rank)
+        # the all-to-all exchange hands this rank exactly its range of every shard
+        a2a = gd.alltoall_states(mine)
+        ok_exchange = ok_exchange and len(a2a) == world and all(
+            same_state(a2a[r], gd.slice_state(states[r], a, b)) for r in range(world))
         parts = [oracle_streams_from_state(gd.slice_state(st, a, b)) for st in states]
         acc = parts[0]
         for other in parts[1:]:
@@ -100,8 +104,9 @@ def _worker(rank, world, port, S, eps, q):
         dist.destroy_process_group()
 
 
-def test_gloo_two_rank_row_shard_fold():
-    S, eps, world = 40, 0.05, 2
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_row_shard_fold(world):
+    S, eps = 40, 0.05
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
