@@ -15,7 +15,11 @@
  *    (e.g. a torch tensor's data_ptr()); "host" pointers are host memory.
  *  - `stream` is a hipStream_t passed as void* (NULL = the default stream).
  *    Work is enqueued on it; calls that return host-visible scalars
- *    (counts, errors) synchronise it before returning.
+ *    (counts, errors) synchronise it before returning.  gk_ingest /
+ *    gk_ingest_quantiles may run part of their work (the sequential
+ *    _sum/_avg chains of streams longer than 16384 values) on a stream the
+ *    set owns; `stream` waits for it before the call returns, so every later
+ *    call enqueued on `stream` sees the finished state.
  *  - A set is not thread-safe.  The library owns the set's device state;
  *    callers own their input and output buffers.
  */
