@@ -1434,12 +1434,98 @@ __device__ __forceinline__ void small_emit(SmallLDS<VPL>& L, int E, int totm, co
   }
 }
 
+// ---- in-register bitonic sort of 128 doubles, two per lane ---------------
+// Position i = lane + 64*r holds a[r].  The partner of a cross-lane
+// compare-exchange (distance j < 64) is lane ^ j: DPP quad_perm for j = 1, 2,
+// ds_swizzle (bitmask mode, no memory access) for j = 4..16, ds_bpermute for
+// j = 32; j = 64 pairs a lane's own two values.  Equal keys keep their own
+// value on both sides (so equal doubles may land in either order -- callers
+// only use this when equal keys are bit-identical).
+template <int J>
+__device__ __forceinline__ int lane_xor_i32(int v, int lane) {
+  if constexpr (J == 1) return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
+  else if constexpr (J == 2) return __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xf, 0xf, false);  // [2,3,0,1]
+  else if constexpr (J < 32) return __builtin_amdgcn_ds_swizzle(v, 0x1F | (J << 10));
+  else return __builtin_amdgcn_ds_bpermute((lane ^ 32) << 2, v);
+}
+
+template <int KB, int J>
+__device__ __forceinline__ void bitonic_stage2(double (&a)[2], int lane) {
+  if constexpr (J == 64) {
+    // positions lane and lane+64 (KB == 128: ascending everywhere)
+    const bool sw = a[1] < a[0];
+    const double lo = sw ? a[1] : a[0], hi = sw ? a[0] : a[1];
+    a[0] = lo;
+    a[1] = hi;
+  } else {
+    const bool lower = (lane & J) == 0;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int i = lane + 64 * r;
+      const bool asc = (i & KB) == 0;
+      const double p = __hiloint2double(lane_xor_i32<J>(__double2hiint(a[r]), lane),
+                                        lane_xor_i32<J>(__double2loint(a[r]), lane));
+      const bool take = (lower == asc) ? (p < a[r]) : (p > a[r]);
+      a[r] = take ? p : a[r];
+    }
+  }
+}
+
+template <int KB, int J>
+__device__ __forceinline__ void bitonic_merge2(double (&a)[2], int lane) {
+  bitonic_stage2<KB, J>(a, lane);
+  if constexpr (J > 1) bitonic_merge2<KB, J / 2>(a, lane);
+}
+
+template <int KB>
+__device__ __forceinline__ void bitonic_sort2(double (&a)[2], int lane) {
+  if constexpr (KB > 2) bitonic_sort2<KB / 2>(a, lane);
+  bitonic_merge2<KB, KB / 2>(a, lane);
+}
+
 // One flush of the small class; K entries per lane (E <= 64*K - 1).  Returns
 // the new table size, or -1 if it would exceed SMALL_CAP-1 (the table is then
 // untouched... except for the counts, which the caller discards).
 template <int VPL, int K, typename AfterSearch>
 __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const double (&xv)[VPL], const int cnt,
                                            const int T, const int lane, AfterSearch&& after_search) {
+  if constexpr (VPL == 2) {
+    // ---- empty table (every stream's first flush): all values are tail
+    //      (gk:85-92), so the flush is a sort and a cut into chunks of
+    //      max(T,1).  Sorted in registers; a flush holding both +0.0 and
+    //      -0.0 (equal keys that differ) takes the exact path below.
+    if (E == 0) {
+      bool pz = false, nz = false;
+#pragma unroll
+      for (int r = 0; r < VPL; ++r) {
+        const bool z = (lane + 64 * r < cnt) && xv[r] == 0.0;
+        pz |= z && !signbit(xv[r]);
+        nz |= z && signbit(xv[r]);
+      }
+      if (!(__builtin_amdgcn_ballot_w64(pz) != 0 && __builtin_amdgcn_ballot_w64(nz) != 0)) {
+        after_search();
+        const CsDiv cd = make_csdiv(T);
+        const int newE = cd.cs > 128 ? (cnt > 0 ? 1 : 0) : cd.div(cnt + cd.cs - 1);
+        if (newE > SMALL_CAP - 1) return -1;
+        double a[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+          a[r] = (lane + 64 * r < cnt) ? xv[r] : __longlong_as_double(0x7ff0000000000000LL);
+        bitonic_sort2<128>(a, lane);
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          const int q = lane + 64 * r;  // rank in the tail
+          const int c = cd.div(q);
+          const int rr = q - c * cd.cs;
+          if (q < cnt && (rr == cd.cs - 1 || q == cnt - 1)) small_put(L, c, a[r], rr + 1, 0);
+        }
+        small_pad(L.tv, newE, lane);
+        wsync<false>();
+        GK_MARK(L, 6);
+        return newE;
+      }
+    }
+  }
   // ---- gap = #entries <= x (gk:93): search from the padded size down ------
   // xb: byte offset of the padded slot of the gap's first entry
   int xb[VPL];
