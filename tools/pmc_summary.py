@@ -49,7 +49,7 @@ def main(d, n_values, streams):
     ing = "k_ingest_small|k_ingest<256"  # the class-256 ingest kernel (current | round-1 name)
     f_ing = avg_of(fetch, fnames, ing)
     w_ing = avg_of(write, wnames, ing)
-    f_st = avg_of(fetch, fnames, "k_stats")
+    f_st = avg_of(fetch, fnames, "k_stats(")  # not k_stats_long (empty launches in cfg3)
     cal = None
     if f_st:
         stats_alg = 8.0 * n_values + 8.0 * (streams + 1) + 40.0 * streams
