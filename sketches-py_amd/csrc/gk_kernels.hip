@@ -1434,53 +1434,66 @@ __device__ __forceinline__ void small_emit(SmallLDS<VPL>& L, int E, int totm, co
   }
 }
 
-// ---- in-register bitonic sort of 128 doubles, two per lane ---------------
-// Position i = lane + 64*r holds a[r].  The partner of a cross-lane
-// compare-exchange (distance j < 64) is lane ^ j: DPP quad_perm for j = 1, 2,
-// ds_swizzle (bitmask mode, no memory access) for j = 4..16, ds_bpermute for
-// j = 32; j = 64 pairs a lane's own two values.  Equal keys keep their own
-// value on both sides (so equal doubles may land in either order -- callers
-// only use this when equal keys are bit-identical).
+// ---- in-register sort of 128 doubles, two per lane ------------------------
+// Position i = lane + 64*r holds a[r].  Bitonic merge sort in the form whose
+// every compare-exchange keeps the smaller key at the lower position: a merge
+// of two ascending runs of KB/2 starts with a mirror stage (i against
+// i ^ (KB-1)), then half-cleaners (i against i ^ J, J = KB/4 .. 1).  The
+// partner lane comes from ds_swizzle (xor within 32 lanes) or ds_bpermute --
+// LDS-pipe instructions, off the VALU, which bounds this kernel; a stage is
+// one compare and two selects per value.  Equal keys may land in either order
+// (callers only use this when equal keys are bit-identical).
 template <int J>
 __device__ __forceinline__ int lane_xor_i32(int v, int lane) {
-  if constexpr (J == 1) return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
-  else if constexpr (J == 2) return __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xf, 0xf, false);  // [2,3,0,1]
-  else if constexpr (J < 32) return __builtin_amdgcn_ds_swizzle(v, 0x1F | (J << 10));
-  else return __builtin_amdgcn_ds_bpermute((lane ^ 32) << 2, v);
+  if constexpr (J < 32) return __builtin_amdgcn_ds_swizzle(v, 0x1F | (J << 10));
+  else return __builtin_amdgcn_ds_bpermute((lane ^ J) << 2, v);
 }
 
-template <int KB, int J>
-__device__ __forceinline__ void bitonic_stage2(double (&a)[2], int lane) {
-  if constexpr (J == 64) {
-    // positions lane and lane+64 (KB == 128: ascending everywhere)
-    const bool sw = a[1] < a[0];
-    const double lo = sw ? a[1] : a[0], hi = sw ? a[0] : a[1];
-    a[0] = lo;
-    a[1] = hi;
-  } else {
-    const bool lower = (lane & J) == 0;
+template <int J>
+__device__ __forceinline__ double lane_xor_f64(double v, int lane) {
+  return __hiloint2double(lane_xor_i32<J>(__double2hiint(v), lane), lane_xor_i32<J>(__double2loint(v), lane));
+}
+
+// a[r] against the value at lane ^ X (same r); the lower lane (bit LB of the
+// lane clear) keeps the minimum
+template <int X, int LB>
+__device__ __forceinline__ void cx_stage2(double (&a)[2], int lane) {
+  const bool lower = (lane & LB) == 0;
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const int i = lane + 64 * r;
-      const bool asc = (i & KB) == 0;
-      const double p = __hiloint2double(lane_xor_i32<J>(__double2hiint(a[r]), lane),
-                                        lane_xor_i32<J>(__double2loint(a[r]), lane));
-      const bool take = (lower == asc) ? (p < a[r]) : (p > a[r]);
-      a[r] = take ? p : a[r];
-    }
+  for (int r = 0; r < 2; ++r) {
+    const double p = lane_xor_f64<X>(a[r], lane);
+    const bool take = (p < a[r]) == lower;
+    a[r] = take ? p : a[r];
   }
 }
 
-template <int KB, int J>
-__device__ __forceinline__ void bitonic_merge2(double (&a)[2], int lane) {
-  bitonic_stage2<KB, J>(a, lane);
-  if constexpr (J > 1) bitonic_merge2<KB, J / 2>(a, lane);
+template <int J>
+__device__ __forceinline__ void half_cleaners2(double (&a)[2], int lane) {
+  cx_stage2<J, J>(a, lane);
+  if constexpr (J > 1) half_cleaners2<J / 2>(a, lane);
 }
 
 template <int KB>
-__device__ __forceinline__ void bitonic_sort2(double (&a)[2], int lane) {
-  if constexpr (KB > 2) bitonic_sort2<KB / 2>(a, lane);
-  bitonic_merge2<KB, KB / 2>(a, lane);
+__device__ __forceinline__ void sort_runs2(double (&a)[2], int lane) {
+  // sorts every aligned run of KB positions (KB <= 64: within each r)
+  if constexpr (KB > 2) sort_runs2<KB / 2>(a, lane);
+  cx_stage2<KB - 1, KB / 2>(a, lane);  // mirror
+  if constexpr (KB >= 4) half_cleaners2<KB / 4>(a, lane);
+}
+
+__device__ __forceinline__ void sort128_2(double (&a)[2], int lane) {
+  sort_runs2<64>(a, lane);  // a[0] and a[1] each ascending over the lanes
+  {
+    // mirror of the full 128: position lane (r=0) against 127-lane, i.e.
+    // lane ^ 63 of r=1; r=0 keeps the minimum
+    const double p0 = lane_xor_f64<63>(a[1], lane);
+    const double p1 = lane_xor_f64<63>(a[0], lane);
+    const bool t0 = p0 < a[0];
+    const bool t1 = a[1] < p1;
+    a[0] = t0 ? p0 : a[0];
+    a[1] = t1 ? p1 : a[1];
+  }
+  half_cleaners2<32>(a, lane);
 }
 
 // One flush of the small class; K entries per lane (E <= 64*K - 1).  Returns
@@ -1511,7 +1524,7 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
 #pragma unroll
         for (int r = 0; r < 2; ++r)
           a[r] = (lane + 64 * r < cnt) ? xv[r] : __longlong_as_double(0x7ff0000000000000LL);
-        bitonic_sort2<128>(a, lane);
+        sort128_2(a, lane);
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
           const int q = lane + 64 * r;  // rank in the tail
