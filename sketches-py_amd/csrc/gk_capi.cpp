@@ -39,6 +39,7 @@ int fail(int code, const char* fmt, ...) {
   } while (0)
 
 constexpr int kCapSmall = GK_SMALL_CAP;  // LDS class (gk_launch.h)
+constexpr int64_t kOvfPrefix = 4096;     // overflow entries read back with the count
 constexpr int kCapLarge = 2048;  // LDS class, ~92 KB per wave
 constexpr int kCapHuge = 32768;  // global-workspace class
 constexpr int kMaxLdsCap = 2048;
@@ -70,8 +71,11 @@ struct gk_set {
   size_t ws_bytes = 0;
   int64_t ws_blocks = 0;
   // overflow reporting
-  int32_t* d_ovf_count = nullptr;
-  int32_t* d_ovf_list = nullptr;
+  int32_t* d_ovf_count = nullptr;  // d_ovf[0]
+  int32_t* d_ovf_list = nullptr;   // d_ovf + 1: one buffer, so count + list come back in one copy
+  int32_t* d_ovf = nullptr;
+  int32_t* h_ovf = nullptr;        // pinned: count + the first kOvfPrefix list entries
+  std::vector<int32_t> h_slots[GK_MAX_CLASSES];  // promotion slots per target class (kept until the next sync)
   int64_t* d_zero_offs = nullptr;  // S+1 zeros: offsets of flush-only launches
   unsigned long long* d_work = nullptr;  // stream hand-out counter of the small-class kernel
   int32_t* d_long_list = nullptr;        // streams k_stats hands to k_stats_long (longest first)
@@ -161,18 +165,24 @@ int sync_list(gk_set* h, int c, hipStream_t stream) {
   return GK_OK;
 }
 
-// Read back the overflow list of the last launch(es); returns count (>= 0) or error.
+// Read back the overflow list of the last launch(es); returns count (>= 0) or
+// error.  The count and the first kOvfPrefix entries come back in one copy
+// (one synchronisation); a longer list takes a second copy.
 int64_t read_overflow(gk_set* h, std::vector<int32_t>& out, hipStream_t stream) {
-  int32_t cnt = 0;
-  if (hipMemcpyAsync(&cnt, h->d_ovf_count, sizeof(int32_t), hipMemcpyDeviceToHost, stream) != hipSuccess ||
+  const int64_t pre = std::min<int64_t>(h->S, kOvfPrefix);
+  if (hipMemcpyAsync(h->h_ovf, h->d_ovf, (1 + pre) * sizeof(int32_t), hipMemcpyDeviceToHost, stream) != hipSuccess ||
       hipStreamSynchronize(stream) != hipSuccess)
     return fail(GK_E_HIP, "overflow readback failed: %s", hipGetErrorString(hipGetLastError()));
+  const int32_t cnt = h->h_ovf[0];
   out.resize(cnt);
   if (cnt) {
-    if (hipMemcpyAsync(out.data(), h->d_ovf_list, cnt * sizeof(int32_t), hipMemcpyDeviceToHost, stream) !=
-            hipSuccess ||
-        hipStreamSynchronize(stream) != hipSuccess)
+    if (cnt <= pre) {
+      std::copy(h->h_ovf + 1, h->h_ovf + 1 + cnt, out.begin());
+    } else if (hipMemcpyAsync(out.data(), h->d_ovf_list, cnt * sizeof(int32_t), hipMemcpyDeviceToHost, stream) !=
+                   hipSuccess ||
+               hipStreamSynchronize(stream) != hipSuccess) {
       return fail(GK_E_HIP, "overflow list readback failed");
+    }
     std::sort(out.begin(), out.end());
   }
   return cnt;
@@ -192,7 +202,10 @@ int promote(gk_set* h, const std::vector<int32_t>& ids, int ncls, hipStream_t st
     rc = ensure_ws(h);
     if (rc) return rc;
   }
-  std::vector<int32_t> slots(ids.size());
+  // host sources of the copies below stay alive until the caller's next
+  // synchronisation (ids: the caller's list; slots: h_slots)
+  std::vector<int32_t>& slots = h->h_slots[ncls];
+  slots.resize(ids.size());
   for (size_t k = 0; k < ids.size(); ++k) slots[k] = (int32_t)(h->slots_used[ncls] + (int64_t)k);
   HIP_TRY(hipMemcpyAsync(h->d_tmp_list, ids.data(), ids.size() * sizeof(int32_t), hipMemcpyHostToDevice, stream));
   HIP_TRY(hipMemcpyAsync(h->d_tmp_slots, slots.data(), slots.size() * sizeof(int32_t), hipMemcpyHostToDevice,
@@ -208,7 +221,6 @@ int promote(gk_set* h, const std::vector<int32_t>& ids, int ncls, hipStream_t st
     h->h_cls[s] = (int8_t)ncls;
     h->members[ncls].push_back(s);
   }
-  HIP_TRY(hipStreamSynchronize(stream));
   for (int c = 1; c < h->st.nclass; ++c) {
     rc = sync_list(h, c, stream);
     if (rc) return rc;
@@ -324,12 +336,9 @@ int run_ingest(gk_set* h, const double* x, const int64_t* offs, int force, hipSt
     HIP_TRY(hipMemsetAsync(h->d_ovf_count, 0, sizeof(int32_t), stream));
     for (int c = 1; c < h->st.nclass; ++c) {
       if (by[c].empty()) continue;
-      int rc = promote(h, by[c], c, stream);
+      int rc = promote(h, by[c], c, stream);  // leaves by[c] in d_tmp_list
       if (rc) return rc;
-      HIP_TRY(hipMemcpyAsync(h->d_tmp_list, by[c].data(), by[c].size() * sizeof(int32_t), hipMemcpyHostToDevice,
-                             stream));
       HIP_TRY(launch_class(h, c, x, offs, h->d_tmp_list, (int64_t)by[c].size(), force, q, stream));
-      HIP_TRY(hipStreamSynchronize(stream));
     }
     cnt = read_overflow(h, ovf, stream);
     if (cnt < 0) return (int)cnt;
@@ -450,8 +459,10 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
   okm &= hipMalloc(&st.slot, S * sizeof(int32_t)) == hipSuccess;
   okm &= hipMalloc(&st.tab[0], (size_t)S * st.cap[0] * sizeof(GKRec)) == hipSuccess;
   okm &= hipMalloc(&st.pbuf, (size_t)S * st.pmax * sizeof(double)) == hipSuccess;
-  okm &= hipMalloc(&h->d_ovf_count, sizeof(int32_t)) == hipSuccess;
-  okm &= hipMalloc(&h->d_ovf_list, S * sizeof(int32_t)) == hipSuccess;
+  okm &= hipMalloc(&h->d_ovf, (S + 1) * sizeof(int32_t)) == hipSuccess;
+  okm &= hipHostMalloc(&h->h_ovf, (std::min<int64_t>(S, kOvfPrefix) + 1) * sizeof(int32_t)) == hipSuccess;
+  h->d_ovf_count = h->d_ovf;
+  h->d_ovf_list = h->d_ovf ? h->d_ovf + 1 : nullptr;
   okm &= hipMalloc(&h->d_zero_offs, (S + 1) * sizeof(int64_t)) == hipSuccess;
   okm &= hipMalloc(&h->d_work, GK_WORK_BYTES) == hipSuccess;
   okm &= hipMalloc(&h->d_long_list, S * sizeof(int32_t)) == hipSuccess;
@@ -494,8 +505,8 @@ int gk_destroy(gk_set* h) {
   GKState& st = h->st;
   void* ptrs[] = {st.n,       st.E,           st.pend,          st.mn,          st.mx,         st.sum,
                   st.avg,     st.cls,         st.slot,          st.tab[0],      st.tab[1],     st.tab[2],
-                  st.pbuf,    h->d_list[0],   h->d_list[1],     h->d_list[2],   h->d_qs,       h->d_ovf_count,
-                  h->d_ovf_list, h->d_tmp_list, h->d_tmp_slots, h->d_ws, h->d_zero_offs, h->d_work,
+                  st.pbuf,    h->d_list[0],   h->d_list[1],     h->d_list[2],   h->d_qs,       h->d_ovf,
+                  h->d_tmp_list, h->d_tmp_slots, h->d_ws, h->d_zero_offs, h->d_work,
                   h->d_long_list, h->d_long_n, h->d_long_count, h->ps.list_ws, h->ps.list_b0, h->ps.ws,
                   h->ps.ws_need};
   for (void* p : ptrs)
@@ -506,6 +517,7 @@ int gk_destroy(gk_set* h) {
   if (h->ev_join) (void)hipEventDestroy(h->ev_join);
   if (h->aux) (void)hipStreamDestroy(h->aux);
   if (h->h_ws_need) (void)hipHostFree(h->h_ws_need);
+  if (h->h_ovf) (void)hipHostFree(h->h_ovf);
   delete h;
   return GK_OK;
 }
@@ -730,13 +742,14 @@ int gk_import(gk_set* h, const int64_t* offs, const double* v, const int32_t* g,
   HIP_TRY(hipMemcpyAsync(h->st.sum, sum, S * sizeof(double), hipMemcpyDeviceToDevice, s));
   HIP_TRY(hipMemcpyAsync(h->st.avg, avg, S * sizeof(double), hipMemcpyDeviceToDevice, s));
   std::vector<int32_t> ovf;
+  std::vector<int32_t> by[GK_MAX_CLASSES];  // outlives the copies promote() enqueues from it
   for (int round = 0; round <= h->st.nclass; ++round) {
     HIP_TRY(hipMemsetAsync(h->d_ovf_count, 0, sizeof(int32_t), s));
     HIP_TRY(gk_launch_import(h->st, offs, v, g, d, poffs, pv, h->d_ovf_count, h->d_ovf_list, s));
     int64_t c = read_overflow(h, ovf, s);
     if (c < 0) return (int)c;
     if (c == 0) return GK_OK;
-    std::vector<int32_t> by[GK_MAX_CLASSES];
+    for (auto& b : by) b.clear();
     for (int32_t id : ovf) {
       const int nc = h->h_cls[id] + 1;
       if (nc >= h->st.nclass)
