@@ -53,6 +53,9 @@ def parse():
                          "default: the whole cfg3 batch")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, os.cpu_count())")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--virtual-shards", type=int, default=1,
+                    help="cfg4 on one process: sketch K row shards on this GPU and fold them with "
+                         "GKArray.merge in shard order (the merge work of a K-GPU run, without the exchange)")
     return ap.parse_args()
 
 
@@ -150,18 +153,31 @@ def main():
         # rows of every stream split over the ranks: this rank sketches its
         # L/world values of each of the S streams, then the shards are merged
         from gkarray_amd import dist as gd
-        L = L // world
-        N = S * L
-        x, offs = make_input(S, L, a.seed + rank, dev, dist_name)
-        ss = StreamSet(S, a.eps, device=dev)
+        K = max(1, a.virtual_shards) if world == 1 else 1
+        L = L // (world * K)
+        N = S * L * K
+        if K == 1:
+            x, offs = make_input(S, L, a.seed + rank, dev, dist_name)
+            ss = StreamSet(S, a.eps, device=dev)
 
-        def step():
-            ss.reset()
-            ss.ingest(x, offs)
-            merged, _ = gd.merge_row_shards(ss)
-            q = merged.quantiles(qs)
-            merged.close()
-            return q
+            def step():
+                ss.reset()
+                ss.ingest(x, offs)
+                merged, _ = gd.merge_row_shards(ss)
+                q = merged.quantiles(qs)
+                merged.close()
+                return q
+        else:
+            shards = [make_input(S, L, a.seed + k, dev, dist_name) for k in range(K)]
+            sets = [StreamSet(S, a.eps, device=dev) for _ in range(K)]
+            ss = sets[0]
+
+            def step():
+                for (xk, ok), sk in zip(shards, sets):
+                    sk.reset()
+                    sk.ingest(xk, ok)
+                sets[0].merge_from(sets[1:])  # sk0.merge(sk1)...merge(skK-1), gk:111-154
+                return sets[0].quantiles(qs)
     else:
         if a.workload == "cfg5":
             x, offs = make_zipf_input(S, 5 + rank, dev, cap=a.values or 10_000_000)
@@ -231,12 +247,13 @@ def main():
                                 % (a.workload, S, ("%d" % L) if a.workload != "cfg5" else
                                    ("clip(zipf(1.5),1,1e7) (%d total)" % N), a.eps, dist_name))
                                if a.workload != "cfg4" else
-                               ("cfg4: %d streams x %d values, row-sharded %d values per stream per GPU, "
-                                "eps=%g, ingest + all-gather + rank-ordered merge + quantiles"
-                                % (S, L * world, L, a.eps)),
+                               ("cfg4: %d streams x %d values, row-sharded %d values per stream per shard "
+                                "(%d GPU x %d shard), eps=%g, ingest + all-to-all + rank-ordered merge + quantiles"
+                                % (S, L * world * K, L, world, K, a.eps)),
                    "streams_per_gpu": S, "values_per_stream": L, "eps": a.eps,
                    "parallelism": ("stream-sharded x%d (no collective)" % world) if a.workload != "cfg4"
-                   else ("row-sharded x%d, RCCL all-gather + merge" % world)},
+                   else ("row-sharded x%d, RCCL all-to-all + merge" % world if K == 1 else
+                         "row-sharded: %d virtual shards on 1 GPU, merge fold (no exchange)" % K)},
         "roofline": {"bound": "hbm", "kernel": "k_ingest", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(a.workload),
                      "bytes_per_launch": bytes_per_launch, "launch_ms": k_ms,

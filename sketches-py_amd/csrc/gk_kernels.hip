@@ -224,7 +224,7 @@ __device__ __forceinline__ GKRec* gk_table_ptr_cs(const GKState& st, int64_t s, 
 // ===========================================================================
 #define STATS_CHUNK 16
 #ifndef GK_STATS_LONG
-#define GK_STATS_LONG 16384  // longer streams go to k_stats_long (one wave each)
+#define GK_STATS_LONG 16384  // longer streams go to k_stats_long (64 per wave, on a second HIP stream)
 #endif
 #define STATS_ROW (STATS_CHUNK + 1)  // +1 double: lanes' rows start on different banks
 
@@ -498,16 +498,118 @@ __global__ __launch_bounds__(256) void k_presort(GKState st, const double* __res
 
 // ===========================================================================
 // k_stats_long: gk:52-59 for the streams k_stats hands over (longer than
-// GK_STATS_LONG values), one wave per stream.  The _avg update is three
-// dependent float64 roundings per value, so a long stream's chain latency
-// sets the time: the wave keeps SL_DEPTH chunks of 64 values in flight
-// (coalesced loads), each lane computes the reciprocal 1.0/n of its value off
-// the chain, and every lane walks the chain over LDS broadcast reads of
-// (v, 1/n) -- identical results in every lane, lane 0 writes them.
-// _min/_max: each lane's first occurrence, reduced by (value, index), then
-// folded into the pre-call values with the strict compares of gk:56-59.
+// GK_STATS_LONG values).  The _avg update is three dependent float64
+// roundings per value, so a long stream's time is its chain latency.  Two
+// layouts, chosen on the device from the list length (the list comes sorted
+// longest first from k_long_prep):
+//  * up to GK_SL_BCAST streams: one wave per stream.  The 64 lanes load 64
+//    consecutive values at a time (coalesced, SL_BCAST_DEPTH chunks in
+//    flight) and compute 64 reciprocals 1.0/n and the first-occurrence
+//    min/max in parallel; every lane walks the chain over LDS broadcast reads
+//    of (v, 1/n), so the chain runs at its latency (~16 ns/value).
+//  * more streams: 64 streams per wave, one per lane, each streaming its own
+//    values into registers (chunks of 16 values as 8 aligned 16-byte loads,
+//    SL_DEPTH chunks in flight).  A step costs ~25 VALU for 64 chains, so
+//    throughput beats one wave per stream once there are more streams than
+//    wave slots (10 000 streams of 10^6 values: cfg4 on one GPU).
+// This kernel runs on a second HIP stream beside k_ingest, which rewrites n:
+// the pre-call n of every listed stream comes from list_n.
 // ===========================================================================
-#define SL_DEPTH 4
+#ifndef GK_SL_BCAST
+#define GK_SL_BCAST 1024
+#endif
+#define SL_BCAST_DEPTH 4
+#ifndef SL_DEPTH
+#define SL_DEPTH 7  // chunks in flight: 7 x 8 loads = 56 <= the 63 vmcnt can count
+#endif
+
+__device__ __forceinline__ void gk_stat_step(double v, int64_t& n, double& sm, double& av, double& mn, double& mx) {
+  n += 1;                                   // gk:52
+  sm = sm + v;                              // gk:53
+  av = av + (v - av) * (1.0 / (double)n);   // gk:54 (no FMA: -ffp-contract=off)
+  if (v < mn) mn = v;                       // gk:56-57 (strict: first occurrence kept)
+  if (v > mx) mx = v;                       // gk:58-59
+}
+
+
+// one wave walks stream list[w] (the broadcast layout)
+__device__ __forceinline__ void stats_long_bcast(const GKState& st, const double* __restrict__ x,
+                                                 const int64_t* __restrict__ offs, const int32_t* __restrict__ list,
+                                                 const int64_t* __restrict__ list_n, int w, int lane, double2* buf) {
+  const int64_t s = list[w];
+  const int64_t xo = offs[s];
+  const int64_t L = offs[s + 1] - xo;
+  int64_t n = list_n[w];
+  double sm = st.sum[s], av = st.avg[s];
+  double lmn = __longlong_as_double(0x7ff0000000000000LL), lmx = -lmn;
+  int64_t imn = INT64_MAX, imx = INT64_MAX;
+  double q[SL_BCAST_DEPTH];
+#pragma unroll
+  for (int d = 0; d < SL_BCAST_DEPTH; ++d) q[d] = (64 * d + lane < L) ? x[xo + 64 * d + lane] : 0.0;
+  for (int64_t k0 = 0; k0 < L; k0 += 64 * SL_BCAST_DEPTH) {
+#pragma unroll
+    for (int d = 0; d < SL_BCAST_DEPTH; ++d) {
+      const int64_t c0 = k0 + 64 * d;  // first index of this chunk
+      if (c0 < L) {
+        const int cn = (int)min((int64_t)64, L - c0);
+        const double v = q[d];
+        if (lane < cn) {
+          const int64_t idx = c0 + lane;
+          if (v < lmn) { lmn = v; imn = idx; }
+          if (v > lmx) { lmx = v; imx = idx; }
+        }
+        buf[lane] = make_double2(v, 1.0 / (double)(n + 1 + lane));
+        const int64_t nx = c0 + 64 * SL_BCAST_DEPTH + lane;  // refill: the chunk SL_BCAST_DEPTH ahead
+        q[d] = (nx < L) ? x[xo + nx] : 0.0;
+        wsync<false>();
+        if (cn == 64) {
+          // keep GK_SL_AHEAD broadcast reads in flight (a ring of registers
+          // refilled as each entry is consumed; sched_barrier pins each
+          // refill before the chain step it hides)
+#ifndef GK_SL_AHEAD
+#define GK_SL_AHEAD 12
+#endif
+          double2 ring[GK_SL_AHEAD];
+#pragma unroll
+          for (int k = 0; k < GK_SL_AHEAD; ++k) ring[k] = buf[k];
+#pragma unroll
+          for (int j = 0; j < 64; ++j) {
+            const double2 e = ring[j % GK_SL_AHEAD];
+            if (j + GK_SL_AHEAD < 64) ring[j % GK_SL_AHEAD] = buf[j + GK_SL_AHEAD];
+            __builtin_amdgcn_sched_barrier(0);
+            sm = sm + e.x;                    // gk:53
+            av = av + (e.x - av) * e.y;       // gk:54
+          }
+        } else {
+          for (int j = 0; j < cn; ++j) {
+            const double2 e = buf[j];
+            sm = sm + e.x;
+            av = av + (e.x - av) * e.y;
+          }
+        }
+        n += cn;  // gk:52
+        wsync<false>();
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double omn = __shfl_xor(lmn, o, 64), omx = __shfl_xor(lmx, o, 64);
+    const int64_t oin = __shfl_xor(imn, o, 64), oix = __shfl_xor(imx, o, 64);
+    if (omn < lmn || (omn == lmn && oin < imn)) { lmn = omn; imn = oin; }
+    if (omx > lmx || (omx == lmx && oix < imx)) { lmx = omx; imx = oix; }
+  }
+  if (lane == 0) {
+    double mn = st.mn[s], mx = st.mx[s];
+    if (lmn < mn) mn = lmn;  // gk:56-57: the pre-call value wins ties
+    if (lmx > mx) mx = lmx;  // gk:58-59
+    st.mn[s] = mn;
+    st.mx[s] = mx;
+    st.sum[s] = sm;
+    st.avg[s] = av;
+  }
+  wsync<false>();
+}
 
 __global__ __launch_bounds__(64) void k_stats_long(GKState st, const double* __restrict__ x,
                                                    const int64_t* __restrict__ offs,
@@ -517,80 +619,84 @@ __global__ __launch_bounds__(64) void k_stats_long(GKState st, const double* __r
   __shared__ double2 buf[64];
   const int lane = threadIdx.x;
   const int cnt = *count;
-  for (int w = blockIdx.x; w < cnt; w += gridDim.x) {
-    const int64_t s = list[w];
-    const int64_t xo = offs[s];
-    const int64_t L = offs[s + 1] - xo;
-    int64_t n = list_n[w];  // pre-call n (k_ingest may already have rewritten st.n[s])
-    double sm = st.sum[s], av = st.avg[s];
-    double lmn = __longlong_as_double(0x7ff0000000000000LL), lmx = -lmn;
-    int64_t imn = INT64_MAX, imx = INT64_MAX;
-    double q[SL_DEPTH];
+  if (cnt <= GK_SL_BCAST) {
+    for (int w = blockIdx.x; w < cnt; w += gridDim.x) stats_long_bcast(st, x, offs, list, list_n, w, lane, buf);
+    return;
+  }
+  const int ngroups = (cnt + 63) / 64;
+  for (int gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
+    const int w = gi * 64 + lane;
+    const bool act = w < cnt;
+    const int64_t s = act ? (int64_t)list[w] : 0;
+    const int64_t xo = act ? offs[s] : 0;
+    int64_t rem = act ? offs[s + 1] - xo : 0;
+    int64_t n = act ? list_n[w] : 0;
+    double mn = 0, mx = 0, sm = 0, av = 0;
+    if (act) {
+      mn = st.mn[s];
+      mx = st.mx[s];
+      sm = st.sum[s];
+      av = st.avg[s];
+    }
+    // peel one value when the stream starts off 16-byte alignment (pointer
+    // arithmetic on x throughout, so the loads stay global_load, not flat)
+    const int64_t peel = (rem > 0 && (((uintptr_t)(x + xo)) & 8)) ? 1 : 0;
+    if (peel) {
+      gk_stat_step(x[xo], n, sm, av, mn, mx);
+      --rem;
+    }
+    const double* p = x + xo + peel;
+    const int64_t nch = rem / 16;  // full chunks of this lane
+    int64_t maxch = nch;
 #pragma unroll
-    for (int d = 0; d < SL_DEPTH; ++d) q[d] = (64 * d + lane < L) ? x[xo + 64 * d + lane] : 0.0;
-    for (int64_t k0 = 0; k0 < L; k0 += 64 * SL_DEPTH) {
+    for (int o = 32; o > 0; o >>= 1) maxch = max(maxch, (int64_t)__shfl_xor(maxch, o, 64));
+    const double2* __restrict__ p2 = (const double2*)p;
+    // loads past a lane's last chunk read the first aligned 16 values of the
+    // batch instead (in bounds: a listed stream alone has > 16384 values), so
+    // every refill load is unconditional and the wait before a slot is
+    // consumed stays partial
+    const double2* __restrict__ dummy = (const double2*)(x + ((((uintptr_t)x) & 8) ? 1 : 0));
+    double2 ring[SL_DEPTH][8];
+#pragma unroll
+    for (int d = 0; d < SL_DEPTH; ++d) {
+      const double2* src = (d < nch) ? p2 + d * 8 : dummy;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ring[d][j] = src[j];
+    }
+    for (int64_t c0 = 0; c0 < maxch; c0 += SL_DEPTH) {
 #pragma unroll
       for (int d = 0; d < SL_DEPTH; ++d) {
-        const int64_t c0 = k0 + 64 * d;  // first index of this chunk
-        if (c0 < L) {
-          const int cn = (int)min((int64_t)64, L - c0);
-          const double v = q[d];
-          if (lane < cn) {
-            const int64_t idx = c0 + lane;
-            if (v < lmn) { lmn = v; imn = idx; }
-            if (v > lmx) { lmx = v; imx = idx; }
-          }
-          buf[lane] = make_double2(v, 1.0 / (double)(n + 1 + lane));
-          const int64_t nx = c0 + 64 * SL_DEPTH + lane;  // refill: the chunk SL_DEPTH ahead
-          q[d] = (nx < L) ? x[xo + nx] : 0.0;
-          wsync<false>();
-          if (cn == 64) {
-            // the chain is latency-bound: keep GK_SL_AHEAD broadcast reads in
-            // flight (a ring of registers refilled as each entry is consumed;
-            // sched_barrier pins each refill before the chain step it hides)
-#ifndef GK_SL_AHEAD
-#define GK_SL_AHEAD 12
-#endif
-            double2 ring[GK_SL_AHEAD];
+        const int64_t c = c0 + d;
+        if (c < nch) {
+          // reciprocals 1.0/n off the chain (IEEE divisions), then the chain
+          double rc[16];
 #pragma unroll
-            for (int k = 0; k < GK_SL_AHEAD; ++k) ring[k] = buf[k];
+          for (int k = 0; k < 16; ++k) rc[k] = 1.0 / (double)(n + 1 + k);
 #pragma unroll
-            for (int j = 0; j < 64; ++j) {
-              const double2 e = ring[j % GK_SL_AHEAD];
-              if (j + GK_SL_AHEAD < 64) ring[j % GK_SL_AHEAD] = buf[j + GK_SL_AHEAD];
-              __builtin_amdgcn_sched_barrier(0);
-              sm = sm + e.x;                    // gk:53
-              av = av + (e.x - av) * e.y;       // gk:54
-            }
-          } else {
-            for (int j = 0; j < cn; ++j) {
-              const double2 e = buf[j];
-              sm = sm + e.x;
-              av = av + (e.x - av) * e.y;
-            }
+          for (int k = 0; k < 16; ++k) {
+            const double v = (k & 1) ? ring[d][k >> 1].y : ring[d][k >> 1].x;
+            sm = sm + v;                    // gk:53
+            av = av + (v - av) * rc[k];     // gk:54
+            if (v < mn) mn = v;             // gk:56-57
+            if (v > mx) mx = v;             // gk:58-59
           }
-          n += cn;  // gk:52
-          wsync<false>();
+          n += 16;                          // gk:52
         }
+        // refill this slot with the chunk SL_DEPTH ahead (unconditional load)
+        const int64_t nx = c + SL_DEPTH;
+        const double2* src = (nx < nch) ? p2 + nx * 8 : dummy;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ring[d][j] = src[j];
       }
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const double omn = __shfl_xor(lmn, o, 64), omx = __shfl_xor(lmx, o, 64);
-      const int64_t oin = __shfl_xor(imn, o, 64), oix = __shfl_xor(imx, o, 64);
-      if (omn < lmn || (omn == lmn && oin < imn)) { lmn = omn; imn = oin; }
-      if (omx > lmx || (omx == lmx && oix < imx)) { lmx = omx; imx = oix; }
-    }
-    if (lane == 0) {
-      double mn = st.mn[s], mx = st.mx[s];
-      if (lmn < mn) mn = lmn;  // gk:56-57: the pre-call value wins ties
-      if (lmx > mx) mx = lmx;  // gk:58-59
+    const int tail = (int)(rem - nch * 16);
+    for (int k = 0; k < tail; ++k) gk_stat_step(p[nch * 16 + k], n, sm, av, mn, mx);
+    if (act) {
       st.mn[s] = mn;
       st.mx[s] = mx;
       st.sum[s] = sm;
       st.avg[s] = av;
     }
-    wsync<false>();
   }
 }
 

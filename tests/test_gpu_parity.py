@@ -429,3 +429,23 @@ def test_fused_query_long_streams_beside_stats(gpu_device):
         ss.ingest(torch.from_numpy(flat), torch.from_numpy(offs))
         osx.ingest(flat, offs)
         assert_same_state(ss, osx, "long plain eps=%g" % eps)
+
+
+def test_many_long_streams_grouped_stats(gpu_device):
+    """More long streams than GK_SL_BCAST (1024): k_stats_long walks them 64
+    per wave, one per lane (register ring of aligned 16-byte loads, one value
+    peeled when a stream starts off 16-byte alignment).  Odd lengths make the
+    starts alternate alignment; two calls carry n, min, max, sum, avg."""
+    rng = np.random.default_rng(47)
+    S = 1100
+    for part in range(2):
+        lens = rng.integers(16385, 19000, S) if part == 0 else rng.integers(16385, 17000, S)
+        if part == 0:
+            ss = _ss(S, 0.01, gpu_device)
+            osx = OracleSet(S, 0.01)
+        seqs = [gen(int(d), int(L), rng) for d, L in zip(rng.integers(0, 8, S), lens)]
+        flat, offs = csr(seqs)
+        got = ss.ingest(torch.from_numpy(flat), torch.from_numpy(offs), quantiles=[0.5, 1.0])
+        osx.ingest(flat, offs)
+        assert_same_quantiles(got.cpu().numpy(), osx.quantiles([0.5, 1.0]), "grouped long q part %d" % part)
+        assert_same_state(ss, osx, "grouped long state part %d" % part)
