@@ -1835,14 +1835,18 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
 
   // ---- stable order inside each gap (gk:72), then emit --------------------
   if (!use_sort) {
-    // Members of a gap are stored in slot order (the atomic slot xs); a
-    // value's rank in its gap counts the members below it, equal members
-    // broken by slot.  The reference breaks ties by insertion order; equal
-    // doubles are bit-identical except +0.0 / -0.0, and a flush holding both
-    // signs of zero takes the exact path below, so the output is the same.
+    // Members of a gap are stored in slot order (the atomic slot xs).  A
+    // value's rank in its gap counts the members below it.  Equal doubles
+    // here are bit-identical (a flush holding both +0.0 and -0.0 takes the
+    // exact path below), so the reference's insertion-order tie-break only
+    // has to give equal values distinct ranks.  Fast pass: strict counts over
+    // every member (self included: never below itself); they are the ranks
+    // iff no gap holds equal values, i.e. iff the rank sum reaches
+    // sum m(m-1)/2 -- otherwise an exact pass (ties broken by slot) reruns.
     int2 gv[VPL];
-    int gb[VPL], mo[VPL], me[VPL];
+    int gb[VPL], mm[VPL], me[VPL];
     int omax = 0;  // this lane's largest member count; the loop runs while any lane needs it
+    int dsum = 0;  // sum over this lane's values of (members - 1)
 #pragma unroll
     for (int r = 0; r < VPL; ++r) {
       const bool v = lane + 64 * r < cnt;
@@ -1850,10 +1854,12 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
       gv[r] = L.gi[gap];
       const int ge = gap < E ? gi_mb(L.gi[gap + 1].x) : totm;
       gb[r] = gi_mb(gv[r].x);
-      mo[r] = v ? ge - gb[r] - 1 : 0;  // other members of the gap
+      const int m = v ? ge - gb[r] : 0;
+      dsum += v ? m - 1 : 0;
+      mm[r] = m >= 2 ? m : 0;  // a lone member has rank 0
       me[r] = (int)xs[r];
       if (v) L.mv[gb[r] + me[r]] = xv[r];
-      omax = max(omax, mo[r]);
+      omax = max(omax, mm[r]);
     }
     wsync<false>();
     int rk[VPL];
@@ -1864,18 +1870,31 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
 #pragma unroll
       for (int r = 0; r < VPL; ++r)
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int u = min(u0 + h, max(mo[r] - 1, 0));
-          y[r][h] = L.mv[min(gb[r] + u + (u >= me[r] ? 1 : 0), 64 * VPL - 1)];
-        }
+        for (int h = 0; h < 2; ++h) y[r][h] = L.mv[gb[r] + min(u0 + h, max(mm[r] - 1, 0))];
 #pragma unroll
       for (int r = 0; r < VPL; ++r)
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int u = u0 + h;
-          const bool below = (y[r][h] < xv[r]) | ((y[r][h] == xv[r]) & (u < me[r]));
-          rk[r] += (u < mo[r] && below) ? 1 : 0;
-        }
+        for (int h = 0; h < 2; ++h) rk[r] += (u0 + h < mm[r] && y[r][h] < xv[r]) ? 1 : 0;
+    }
+    int rsum = 0;
+#pragma unroll
+    for (int r = 0; r < VPL; ++r) rsum += rk[r];
+    // (DPP scan: the sum wraps mod 2^32, exact for these small counts)
+    if (__builtin_amdgcn_readlane((int)wave_incl_scan_u32((uint32_t)(2 * rsum - dsum), lane), 63) != 0) {
+      // equal values in some gap: exact ranks, ties broken by slot
+#pragma unroll
+      for (int r = 0; r < VPL; ++r) rk[r] = 0;
+      for (int u0 = 0; __builtin_amdgcn_ballot_w64(u0 < omax) != 0; u0 += 2) {
+#pragma unroll
+        for (int r = 0; r < VPL; ++r)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int u = u0 + h;
+            const double yy = L.mv[gb[r] + min(u, max(mm[r] - 1, 0))];
+            const bool below = (yy < xv[r]) | ((yy == xv[r]) & (u < me[r]));
+            rk[r] += (u < mm[r] && below) ? 1 : 0;
+          }
+      }
     }
 #pragma unroll
     for (int r = 0; r < VPL; ++r)
