@@ -1480,8 +1480,14 @@ __device__ __forceinline__ void small_zero_counts(uint32_t* gpk, int lane) {
 }
 
 __device__ __forceinline__ void small_pad(double* tv, int E, int lane) {
-  const int hi = gk_pow2_above(E) - 1;
-  for (int j = E + lane; j < hi; j += 64) tv[pidx(j)] = __longlong_as_double(0x7ff0000000000000LL);
+  if constexpr (SMALL_CAP == 128) {
+    // slots E .. pow2_above(E)-2 lie inside E .. E+63 (E <= 127); one store
+    // per lane, clamped to slot 127, which never holds an entry
+    tv[pidx(min(E + lane, SMALL_CAP - 1))] = __longlong_as_double(0x7ff0000000000000LL);
+  } else {
+    const int hi = gk_pow2_above(E) - 1;
+    for (int j = E + lane; j < hi; j += 64) tv[pidx(j)] = __longlong_as_double(0x7ff0000000000000LL);
+  }
 }
 
 // a / cs for 0 <= a < 256, cs = max(T,1) >= 1: cs == 1 -> a, cs >= 256 -> 0,
