@@ -51,17 +51,20 @@ def small_isa(tmp_path_factory):
 
 
 def test_fast_class_has_no_scratch(resource_report, small_isa):
-    """The 256-entry class runs nearly every stream: no scratch traffic in the
-    flush path.  The allocator folds at most two per-lane base addresses of the
-    end-of-stream pending copy into scratch (one store each at kernel entry, one
-    reload each per stream); anything more is a spill in the hot loop."""
+    """The small class runs nearly every stream: no scratch traffic in the
+    per-flush path.  The allocator folds a few loop-invariant per-lane LDS /
+    global addresses into scratch: stored once at kernel entry, reloaded once
+    per stream (end-of-stream pending copy, the empty-table first flush).
+    Keeping them in registers instead (e.g. re-reading the gap info at emit)
+    measured 1-2% slower (profiles/r01t_ab_regpressure_REJECTED.txt), so the
+    bound is on the count: a spill inside the flush loops adds many more."""
     fast = {k: v for k, v in resource_report.items() if k.startswith("_Z14k_ingest_small")}
     assert len(fast) == 2
     for k, v in fast.items():
         assert v.get("ScratchSize [bytes/lane]", 0) <= 32, (k, v)
     for name, body in small_isa.items():
         ops = re.findall(r"^\s*(scratch_\w+)", body, re.M)
-        assert len(ops) <= 8, (name, ops)
+        assert len(ops) <= 10, (name, ops)
 
 
 def test_no_inline_asm_memory_ops():
