@@ -53,6 +53,8 @@ def parse():
                          "default: the whole cfg3 batch")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, os.cpu_count())")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--exchange", default="allgather", choices=["allgather", "alltoall"],
+                    help="cfg4 row-shard exchange over RCCL before the merge fold")
     ap.add_argument("--virtual-shards", type=int, default=1,
                     help="cfg4 on one process: sketch K row shards on this GPU and fold them with "
                          "GKArray.merge in shard order (the merge work of a K-GPU run, without the exchange)")
@@ -163,7 +165,7 @@ def main():
             def step():
                 ss.reset()
                 ss.ingest(x, offs)
-                merged, _ = gd.merge_row_shards(ss)
+                merged, _ = gd.merge_row_shards(ss, exchange=a.exchange)
                 q = merged.quantiles(qs)
                 merged.close()
                 return q
@@ -248,11 +250,11 @@ def main():
                                    ("clip(zipf(1.5),1,1e7) (%d total)" % N), a.eps, dist_name))
                                if a.workload != "cfg4" else
                                ("cfg4: %d streams x %d values, row-sharded %d values per stream per shard "
-                                "(%d GPU x %d shard), eps=%g, ingest + all-to-all + rank-ordered merge + quantiles"
-                                % (S, L * world * K, L, world, K, a.eps)),
+                                "(%d GPU x %d shard), eps=%g, ingest + %s + rank-ordered merge + quantiles"
+                                % (S, L * world * K, L, world, K, a.eps, a.exchange)),
                    "streams_per_gpu": S, "values_per_stream": L, "eps": a.eps,
                    "parallelism": ("stream-sharded x%d (no collective)" % world) if a.workload != "cfg4"
-                   else ("row-sharded x%d, RCCL all-to-all + merge" % world if K == 1 else
+                   else ("row-sharded x%d, RCCL %s + merge" % (world, a.exchange) if K == 1 else
                          "row-sharded: %d virtual shards on 1 GPU, merge fold (no exchange)" % K)},
         "roofline": {"bound": "hbm", "kernel": "k_ingest", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(a.workload),

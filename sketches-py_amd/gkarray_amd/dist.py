@@ -10,10 +10,11 @@ Two ways streams meet several GPUs:
   ``sk_0.merge(sk_1) ... .merge(sk_{N-1})`` (gk:111-154).  ``merge_row_shards``
   hands every rank the N shard states of the streams of its own range and the
   rank folds them in rank order -- the merge work is split N ways and the
-  result is stream-sharded.  The default exchange is an all-to-all
-  (``alltoall_states``: rank r sends each peer only that peer's stream range,
-  so every table crosses xGMI once); ``exchange="allgather"`` moves every
-  rank's whole state to every rank (N-1 times the bytes).
+  result is stream-sharded.  The default exchange is the all-gather the
+  north star names (every rank's whole state to every rank);
+  ``exchange="alltoall"`` (``alltoall_states``: rank r sends each peer only
+  that peer's stream range, so every table crosses xGMI once) moves 1/(N-1)
+  of the bytes -- SURVEY 8(f)'s next step, same fold, same results.
 
 The exchange helpers (``pack_state`` / ``unpack_state`` / ``all_gather_varlen``
 / ``allgather_states`` / ``alltoall_states`` / ``slice_state``) work on tensors of any device, so the
@@ -173,13 +174,13 @@ def fold_states(states, device=None):
     return acc
 
 
-def merge_row_shards(ss, group=None, exchange="alltoall"):
+def merge_row_shards(ss, group=None, exchange="allgather"):
     """Row-sharded sketches -> merged sketches of this rank's stream range.
 
     `ss` is this rank's StreamSet over all S streams (built from its slice of
     the rows).  Returns (StreamSet over streams [a, b), (a, b)); the fold is in
     rank order, identical to the reference's sk0.merge(sk1)...merge(skN-1).
-    `exchange`: "alltoall" (each table crosses once) or "allgather".
+    `exchange`: "allgather" (north star) or "alltoall" (each table crosses once).
     """
     if exchange not in ("alltoall", "allgather"):
         raise ValueError("exchange must be 'alltoall' or 'allgather'")
