@@ -2449,45 +2449,121 @@ __global__ __launch_bounds__(64) void k_merge(MergeArgs a) {
       m.td[j] = rc.d;
     }
     __syncthreads();
-    // ---- the four-rule walk of gk:76-106, on lane 0 ---------------------------
-    if (lane == 0) {
+    // ---- the four-rule walk of gk:76-106, wave-parallel ----------------------
+    // Incoming records (sorted) fall into gaps: record i precedes entry j iff
+    // iv[i] < tv[j] (gk:93), so gap j holds [a_{j-1}, a_j) with a_j = #{i :
+    // iv[i] < tv[j]}, and the tail [a_{E-1}, M) follows the last entry.  Entry
+    // j with carry-in c (the g of removed predecessors, gk:80/102) starts at
+    // G = g_j + c and walks its gap in order: record i is absorbed iff
+    // g_i + G + d_j <= T (G += g_i), else emitted as (v_i, g_i, G + d_j - g_i)
+    // (gk:94-99); the entry is then removed (carry G) iff j+1 < E and
+    // G + g_{j+1} + d_{j+1} <= T (gk:79/101), else emitted as (v_j, G, d_j).
+    // The tail chains records (gk:86-92).  Lane l owns entries [lK, lK+K); the
+    // carries are resolved by rounds (each lane re-walks its block from its
+    // left neighbour's last carry-out) until no carry-in changes -- lane 0's is
+    // fixed, so the fixpoint is the sequential walk.  Then counts, a wave scan
+    // and a second walk write the records in order.
+    {
       const int64_t T = (int64_t)floor(st.two_eps * (double)(n - 1));  // gk:70
       const int M = p + nrec;
-      int i = 0, j = 0, no = 0;
-      bool of = false;
-      while (i < M || j < E) {
-        bool emit = false;
-        double ev = 0.0;
-        int64_t eg = 0, ed = 0;
-        if (i < M && (j == E || m.iv[i] < m.tv[j])) {
-          if (j == E) {  // gk:85-92
-            if (i + 1 < M && (int64_t)m.ig[i] + m.ig[i + 1] + m.id[i + 1] <= T) {
-              m.ig[i + 1] += m.ig[i];
-            } else {
-              emit = true; ev = m.iv[i]; eg = m.ig[i]; ed = m.id[i];
-            }
-          } else {  // gk:93-99
-            if ((int64_t)m.ig[i] + m.tg[j] + m.td[j] <= T) {
-              m.tg[j] += m.ig[i];
-            } else {
-              emit = true; ev = m.iv[i]; eg = m.ig[i]; ed = (int64_t)m.tg[j] + m.td[j] - m.ig[i];
-            }
-          }
-          ++i;
-        } else {  // gk:77-84, gk:100-106
-          if (j + 1 < E && (int64_t)m.tg[j] + m.tg[j + 1] + m.td[j + 1] <= T) {
-            m.tg[j + 1] += m.tg[j];
-          } else {
-            emit = true; ev = m.tv[j]; eg = m.tg[j]; ed = m.td[j];
-          }
-          ++j;
+      int32_t* ga = m.rg;  // a_j (records are in iv/ig/id by now)
+      for (int j = lane; j < E; j += 64) {
+        const double tvj = m.tv[j];
+        int lo = 0, hi = M;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (m.iv[mid] < tvj) lo = mid + 1; else hi = mid;
         }
-        if (emit) {
-          if (no >= outcap) { of = true; break; }
-          m.ov[no] = ev; m.og[no] = (int32_t)eg; m.od[no] = (int32_t)ed; ++no;
+        ga[j] = lo;
+      }
+      __syncthreads();
+      const int K = (E + 63) >> 6;
+      const int j0 = lane * K;
+      const int jend = min(j0 + K, E);
+      // walk of the lane's block from carry-in c; returns the carry-out and
+      // the number of records it emits (out != NULL: also writes them)
+      auto walk = [&](int64_t c, int& cnt_out, int obase, bool write) -> int64_t {
+        int no_l = 0;
+        for (int j = j0; j < jend; ++j) {
+          int64_t G = (int64_t)m.tg[j] + c;
+          const int64_t dj = m.td[j];
+          const int ib = j == 0 ? 0 : ga[j - 1];
+          const int ie = ga[j];
+          for (int i = ib; i < ie; ++i) {
+            const int64_t gi = m.ig[i];
+            if (gi + G + dj <= T) {
+              G += gi;
+            } else {
+              if (write) {
+                m.ov[obase + no_l] = m.iv[i];
+                m.og[obase + no_l] = (int32_t)gi;
+                m.od[obase + no_l] = (int32_t)(G + dj - gi);
+              }
+              ++no_l;
+            }
+          }
+          const bool rem = (j + 1 < E) && (G + m.tg[j + 1] + m.td[j + 1] <= T);
+          if (rem) {
+            c = G;
+          } else {
+            if (write) {
+              m.ov[obase + no_l] = m.tv[j];
+              m.og[obase + no_l] = (int32_t)G;
+              m.od[obase + no_l] = (int32_t)dj;
+            }
+            ++no_l;
+            c = 0;
+          }
+        }
+        cnt_out = no_l;
+        return c;
+      };
+      int64_t cin = 0;
+      int cnt_blk = 0;
+      for (int round = 0; round <= 64; ++round) {
+        const int64_t cout = walk(cin, cnt_blk, 0, false);
+        int64_t ncin = __shfl_up(cout, 1, 64);
+        if (lane == 0) ncin = 0;
+        if (__ballot(ncin != cin) == 0) break;
+        cin = ncin;
+      }
+      // the tail (gk:85-92), on the lane owning the last entry
+      const int tail_lane = E == 0 ? 0 : (E - 1) / K;
+      const int t0 = E == 0 ? 0 : ga[E - 1];
+      int cnt_tail = 0;
+      if (lane == tail_lane) {
+        int64_t acc = 0;
+        for (int i = t0; i < M; ++i) {
+          acc += m.ig[i];
+          if (i + 1 < M && acc + m.ig[i + 1] + m.id[i + 1] <= T) continue;  // into record i+1
+          ++cnt_tail;
+          acc = 0;
         }
       }
-      sh_out = of ? -1 : no;
+      const int mine = (j0 < E ? cnt_blk : 0) + cnt_tail;
+      const uint32_t incl = wave_incl_scan_u32((uint32_t)mine, lane);
+      const int total = __builtin_amdgcn_readlane((int)incl, 63);
+      if (total > outcap) {
+        if (lane == 0) sh_out = -1;
+      } else {
+        const int obase = (int)incl - mine;
+        int wrote = 0;
+        if (j0 < E) walk(cin, wrote, obase, true);
+        if (lane == tail_lane) {
+          int o = obase + wrote;
+          int64_t acc = 0;
+          for (int i = t0; i < M; ++i) {
+            acc += m.ig[i];
+            if (i + 1 < M && acc + m.ig[i + 1] + m.id[i + 1] <= T) continue;
+            m.ov[o] = m.iv[i];
+            m.og[o] = (int32_t)acc;
+            m.od[o] = m.id[i];
+            ++o;
+            acc = 0;
+          }
+        }
+        if (lane == 0) sh_out = total;
+      }
     }
     __syncthreads();
     const int no = sh_out;

@@ -449,3 +449,46 @@ def test_many_long_streams_grouped_stats(gpu_device):
         osx.ingest(flat, offs)
         assert_same_quantiles(got.cpu().numpy(), osx.quantiles([0.5, 1.0]), "grouped long q part %d" % part)
         assert_same_state(ss, osx, "grouped long state part %d" % part)
+
+
+@pytest.mark.parametrize("eps", [0.05, 0.01, 0.001])
+def test_merge_compress_records_vs_oracle(gpu_device, eps):
+    """merge_compress(entries) with explicit (v, g, delta) records (gk:63-109):
+    arbitrary g and delta exercise every rule of the wave-parallel walk
+    (absorption by the running g, the removal carry, the tail chain), with
+    pending values, ties between records and entries, and empty sides."""
+    from gk_oracle import OracleGK
+    rng = np.random.default_rng(53 + int(1 / eps))
+    S = 240
+    P = int(1.0 / eps) + 1
+    lens = rng.integers(0, 4 * P, S)
+    lens[:4] = [0, 1, P, P + 7]
+    seqs = [gen(int(d), int(L), rng) for d, L in zip(rng.integers(0, 8, S), lens)]
+    ss = _ss(S, eps, gpu_device)
+    ingest_np(ss, seqs)
+    ors = []
+    for sq in seqs:
+        o = OracleGK(eps)
+        o.add_many(sq)
+        ors.append(o)
+    vals, gs, ds, offs = [], [], [], [0]
+    recs_all = []
+    for s in range(S):
+        k = int(rng.integers(0, 60))
+        if s % 7 == 0:
+            k = 0
+        base = seqs[s] if len(seqs[s]) else rng.random(4)
+        v = np.sort(np.concatenate([rng.choice(base, size=k // 2), rng.lognormal(0, 1, k - k // 2)]))
+        g = rng.integers(1, 3 + int(0.02 / eps), k)
+        d = rng.integers(0, 2 + int(0.04 / eps), k)
+        recs = list(zip(v.tolist(), g.tolist(), d.tolist()))
+        recs_all.append(recs)
+        vals += v.tolist(); gs += g.tolist(); ds += d.tolist(); offs.append(offs[-1] + k)
+    ss.merge_compress(torch.tensor(vals, dtype=torch.float64), torch.tensor(gs, dtype=torch.int32),
+                      torch.tensor(ds, dtype=torch.int32), torch.tensor(offs, dtype=torch.int64))
+    to, tv, tg, td = (t.cpu() for t in ss.tables())
+    for s in range(S):
+        ors[s].flush(recs_all[s])
+        a, b = int(to[s]), int(to[s + 1])
+        got = list(zip(tv[a:b].tolist(), tg[a:b].tolist(), td[a:b].tolist()))
+        assert got == ors[s].table(), "stream %d eps=%g" % (s, eps)
