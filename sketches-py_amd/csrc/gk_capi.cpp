@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -42,6 +43,7 @@ constexpr int kCapSmall = GK_SMALL_CAP;  // LDS class (gk_launch.h)
 constexpr int64_t kOvfPrefix = 4096;     // overflow entries read back with the count
 constexpr int kCapLarge = 2048;  // LDS class, ~92 KB per wave
 constexpr int kCapHuge = 32768;  // global-workspace class
+constexpr int64_t kRecipTable = (int64_t)1 << 17;  // entries of st.rtab (1 MiB)
 constexpr int kMaxLdsCap = 2048;
 
 int vpl_for(int P) {
@@ -95,6 +97,9 @@ struct gk_set {
   int32_t* d_tmp_list = nullptr;
   int32_t* d_tmp_slots = nullptr;
   int64_t tmp_alloc = 0;
+  // quarter waves per CU of the small-class batch launch that walk the gk:52-59
+  // stats chains first (0: separate k_stats launch); GK_FUSED_STATS overrides
+  int fused_stats = 3;
   // timing
   bool timing = false;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -233,12 +238,15 @@ int check_set(const gk_set* h) {
   return GK_OK;
 }
 
+bool stats_fused(const gk_set* h);
+
 hipError_t launch_class(gk_set* h, int c, const double* x, const int64_t* offs, const int32_t* list, int64_t count,
                         int force, const GKQuery& q, hipStream_t stream, bool prio = false) {
   return gk_launch_ingest(h->st.cap[c], h->vpl, h->st, x, offs, list, count, force, h->d_ws, h->ws_bytes,
                           h->ws_blocks, h->d_ovf_count, h->d_ovf_list, q, h->d_work,
                           prio ? h->d_long_list : nullptr, prio ? h->d_long_count : nullptr,
-                          prio && h->ps.ws ? h->ps.ws : nullptr, prio && h->ps.ws ? h->ps.list_ws : nullptr, stream);
+                          prio && h->ps.ws ? h->ps.ws : nullptr, prio && h->ps.ws ? h->ps.list_ws : nullptr,
+                          (prio && c == 0 && stats_fused(h)) ? h->fused_stats : 0, stream);
 }
 
 // gk:52-59 for a batch: k_stats over every stream on `s` (it lists the
@@ -247,12 +255,17 @@ hipError_t launch_class(gk_set* h, int c, const double* x, const int64_t* offs, 
 // that follow on `s` (they touch neither _sum nor _avg).  stats_join makes
 // `s` wait for them and, for a fused query, re-answers the long streams with
 // their final _min/_max.
+// the small-class batch launch walks the stats chains itself (k_stats then
+// only lists the long streams)
+bool stats_fused(const gk_set* h) { return h->fused_stats > 0 && h->st.cap[0] == GK_SMALL_CAP; }
+
 int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s) {
   if (h->timing) HIP_TRY(hipEventRecord(h->ev[2], s));
   // k_stats + k_long_prep, then the fork (k_stats_long needs only the
   // sorted list and the pre-call n), then the presort of the long streams'
   // flush batches on `s`
-  HIP_TRY(gk_launch_stats(h->st, x, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->ps, s));
+  HIP_TRY(gk_launch_stats(h->st, x, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->ps,
+                          stats_fused(h) ? 1 : 0, s));
   HIP_TRY(hipEventRecord(h->ev_fork, s));
   HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_fork, 0));
   HIP_TRY(gk_launch_stats_long(h->st, x, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->aux));
@@ -420,6 +433,7 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
   h->P = (int)inv + 1;  // gk:60
   h->device = device;
   h->vpl = vpl_for(h->P);
+  if (const char* fs = getenv("GK_FUSED_STATS")) h->fused_stats = std::max(0, std::min(32, atoi(fs)));
   GKState& st = h->st;
   st.S = num_streams;
   st.eps = eps;
@@ -459,6 +473,8 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
   okm &= hipMalloc(&st.slot, S * sizeof(int32_t)) == hipSuccess;
   okm &= hipMalloc(&st.tab[0], (size_t)S * st.cap[0] * sizeof(GKRec)) == hipSuccess;
   okm &= hipMalloc(&st.pbuf, (size_t)S * st.pmax * sizeof(double)) == hipSuccess;
+  st.rtab_n = kRecipTable;
+  okm &= hipMalloc(&st.rtab, (size_t)st.rtab_n * sizeof(double)) == hipSuccess;
   okm &= hipMalloc(&h->d_ovf, (S + 1) * sizeof(int32_t)) == hipSuccess;
   okm &= hipHostMalloc(&h->h_ovf, (std::min<int64_t>(S, kOvfPrefix) + 1) * sizeof(int32_t)) == hipSuccess;
   h->d_ovf_count = h->d_ovf;
@@ -490,6 +506,7 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
   if (hipMemset(st.cls, 0, S * sizeof(int32_t)) != hipSuccess ||
       hipMemset(h->d_zero_offs, 0, (S + 1) * sizeof(int64_t)) != hipSuccess ||
       hipMemset(st.slot, 0, S * sizeof(int32_t)) != hipSuccess || gk_launch_reset(st, nullptr) != hipSuccess ||
+      gk_launch_rtab(st, nullptr) != hipSuccess ||
       hipDeviceSynchronize() != hipSuccess) {
     gk_destroy(h);
     return fail(GK_E_HIP, "state initialisation failed");
@@ -508,7 +525,7 @@ int gk_destroy(gk_set* h) {
                   st.pbuf,    h->d_list[0],   h->d_list[1],     h->d_list[2],   h->d_qs,       h->d_ovf,
                   h->d_tmp_list, h->d_tmp_slots, h->d_ws, h->d_zero_offs, h->d_work,
                   h->d_long_list, h->d_long_n, h->d_long_count, h->ps.list_ws, h->ps.list_b0, h->ps.ws,
-                  h->ps.ws_need};
+                  h->ps.ws_need, st.rtab};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (auto& e : h->ev)

@@ -20,6 +20,9 @@
 #include <stdint.h>
 #include <math.h>
 
+#include <algorithm>
+#include <type_traits>
+
 #include "gk_state.h"
 #include "gk_launch.h"
 
@@ -230,7 +233,8 @@ __device__ __forceinline__ GKRec* gk_table_ptr_cs(const GKState& st, int64_t s, 
 
 __global__ __launch_bounds__(256) void k_stats(GKState st, const double* __restrict__ x,
                                                const int64_t* __restrict__ offs,
-                                               int32_t* __restrict__ long_list, int32_t* __restrict__ long_count) {
+                                               int32_t* __restrict__ long_list, int32_t* __restrict__ long_count,
+                                               int lengths_only) {
   __shared__ double tile[256 * STATS_ROW];
   __shared__ int64_t so[257];
   __shared__ int64_t smax;
@@ -253,7 +257,8 @@ __global__ __launch_bounds__(256) void k_stats(GKState st, const double* __restr
   atomicMax((unsigned long long*)&smax, (unsigned long long)L);
   __syncthreads();
   const int64_t maxL = smax;
-  if (maxL == 0) return;
+  // lengths only: the long list; the chains run in the small-class launch
+  if (maxL == 0 || lengths_only) return;
   const int64_t s = s0 + t;
   int64_t n = 0;
   double mn = 0, mx = 0, sm = 0, av = 0;
@@ -2044,6 +2049,131 @@ __device__ __attribute__((noinline)) void small_quantiles(SmallLDS<VPL>& L, int 
   }
 }
 
+// ---- stats role of the small-class launch (gk:52-59) ----------------------
+// The ingest waves are VALU/SALU-issue-bound and leave most of the HBM
+// bandwidth idle, while k_stats is a pure stream of the same values; run as a
+// separate launch it cost ~19% of a cfg3 step and cannot share the CUs with
+// the persistent ingest grid (profiles/r01c_ab_concurrent_stats.txt).  So the
+// first `nstat` waves of the small-class launch walk the _sum/_avg chains
+// first -- 64 streams per wave, one per lane, from a register ring of aligned
+// 16-byte loads (the k_stats_long layout, shallower) -- and then join the
+// ingest hand-out.  Batches of 64 streams are handed out through `swork`.
+// Streams longer than GK_STATS_LONG are k_stats_long's (listed beforehand by
+// the lengths-only k_stats).  The ingest waves do not read _min/_max: a fused
+// query that needs them writes a marker that k_qfix resolves after the launch.
+#ifndef GK_FS_DEPTH
+#define GK_FS_DEPTH 2  // chunks of 8 values in flight per lane
+#endif
+#define GK_SWORK_IDX 128  // the stats batch counter in `work` (after the 8 ingest parts)
+#define GK_QMARK_MIN 0x7ff4000000000001LL  // quantile = _min of the stream (gk:182-183, 220)
+#define GK_QMARK_MAX 0x7ff4000000000002LL  // quantile = _max of the stream (gk:229)
+
+__device__ __forceinline__ void fused_stats_role(const GKState& st, const double* __restrict__ x,
+                                                 const int64_t* __restrict__ offs,
+                                                 unsigned long long* __restrict__ swork, int lane) {
+  const int64_t nb = (st.S + 63) / 64;
+  const double2* __restrict__ dummy = (const double2*)(x + ((((uintptr_t)x) & 8) ? 1 : 0));
+  for (;;) {
+    unsigned long long v = 0;
+    if (lane == 0) v = atomicAdd(swork, 1ull);
+    const int64_t b = rfl64((int64_t)v);
+    if (b >= nb) break;
+    const int64_t s = b * 64 + lane;
+    const bool live = s < st.S;
+    const int64_t xo = live ? offs[s] : 0;
+    int64_t rem = live ? offs[s + 1] - xo : 0;
+    if (rem > GK_STATS_LONG) rem = 0;  // k_stats_long's
+    const bool act = rem > 0;
+    int64_t n = 0;
+    double mn = 0, mx = 0, sm = 0, av = 0;
+    if (act) {
+      n = st.n[s];
+      mn = st.mn[s];
+      mx = st.mx[s];
+      sm = st.sum[s];
+      av = st.avg[s];
+    }
+    // peel one value when the stream starts off 16-byte alignment
+    const int64_t peel = (act && (((uintptr_t)(x + xo)) & 8)) ? 1 : 0;
+    if (peel) {
+      gk_stat_step(x[xo], n, sm, av, mn, mx);
+      --rem;
+    }
+    const double* p = x + xo + peel;
+    const int64_t nch = rem / 8;  // full chunks of 8 values
+    int64_t maxch = nch;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) maxch = max(maxch, (int64_t)__shfl_xor(maxch, o, 64));
+    const double2* __restrict__ p2 = (const double2*)p;
+    // Streams of one batch usually share n (same history): the gk:54 factors
+    // 1.0/n are then wave-uniform and read from st.rtab (scalar loads)
+    // instead of ~10 VALU of IEEE division per value.  n of the active lanes
+    // stays equal chunk by chunk (each adds 8 per chunk while active).
+    int64_t nlo = act ? n : INT64_MAX, nhi = act ? n : INT64_MIN;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      nlo = min(nlo, (int64_t)__shfl_xor(nlo, o, 64));
+      nhi = max(nhi, (int64_t)__shfl_xor(nhi, o, 64));
+    }
+    const int64_t nu = rfl64(nlo);
+    const bool uni = nu == rfl64(nhi) && nu >= 0 && nu + 8 * maxch + 8 < st.rtab_n;
+    // loads past a lane's last chunk read the first aligned values of the
+    // batch instead, so every refill is unconditional
+    double2 ring[GK_FS_DEPTH][4];
+#pragma unroll
+    for (int d = 0; d < GK_FS_DEPTH; ++d) {
+      const double2* src = (d < nch) ? p2 + d * 4 : dummy;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ring[d][j] = src[j];
+    }
+    auto walk = [&](auto tab) {
+      constexpr bool TAB = decltype(tab)::value;
+      for (int64_t c0 = 0; c0 < maxch; c0 += GK_FS_DEPTH) {
+#pragma unroll
+        for (int d = 0; d < GK_FS_DEPTH; ++d) {
+          const int64_t c = c0 + d;
+          if (c < nch) {
+            const double* __restrict__ rt = st.rtab + (nu + 8 * c + 1);  // uniform (TAB)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const double v = (k & 1) ? ring[d][k >> 1].y : ring[d][k >> 1].x;
+              const double rc = TAB ? rt[k] : 1.0 / (double)(n + 1 + k);  // off the chain
+              sm = sm + v;                    // gk:53
+              av = av + (v - av) * rc;        // gk:54
+              if (v < mn) mn = v;             // gk:56-57
+              if (v > mx) mx = v;             // gk:58-59
+            }
+            n += 8;                           // gk:52
+          }
+          const int64_t nx = c + GK_FS_DEPTH;
+          const double2* src = (nx < nch) ? p2 + nx * 4 : dummy;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) ring[d][j] = src[j];
+        }
+      }
+    };
+    if (uni) walk(std::true_type{});
+    else walk(std::false_type{});
+    const int tail = (int)(rem - nch * 8);
+    for (int k = 0; k < tail; ++k) gk_stat_step(p[nch * 8 + k], n, sm, av, mn, mx);
+    if (act) {
+      st.mn[s] = mn;
+      st.mx[s] = mx;
+      st.sum[s] = sm;
+      st.avg[s] = av;
+    }
+  }
+}
+
+// fused-stats launches: quantiles that are _min / _max (markers) resolved
+__global__ void k_qfix(GKState st, double* __restrict__ out, int nq) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= st.S * (int64_t)nq) return;
+  const long long b = __double_as_longlong(out[i]);
+  if (b == GK_QMARK_MIN) out[i] = st.mn[i / nq];
+  else if (b == GK_QMARK_MAX) out[i] = st.mx[i / nq];
+}
+
 template <int VPL>
 __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st, const double* __restrict__ x,
                                                      const int64_t* __restrict__ offs,
@@ -2051,10 +2181,11 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
                                                      int32_t* __restrict__ ovf_count, int32_t* __restrict__ ovf_list,
                                                      const double* __restrict__ qs, int nq,
                                                      double* __restrict__ qout, int qmode,
-                                                     unsigned long long* __restrict__ work) {
+                                                     unsigned long long* __restrict__ work, int nstat) {
   __shared__ __attribute__((aligned(16))) SmallLDS<VPL> L;
   const int lane = threadIdx.x;
   const int P = st.P;
+    if ((int)blockIdx.x < nstat) fused_stats_role(st, x, offs, work + GK_SWORK_IDX, lane);
 #ifdef GK_PROF
   if (lane == 0) {
     for (int i = 0; i < GK_PROF_NSEC; ++i) L.prof[i] = 0;
@@ -2097,8 +2228,11 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
     int64_t n = rfl64(hv.n);
     const int64_t xo = rfl64(hv.xo);
     const int64_t xe = rfl64(hv.xe);
-    const double smn = __longlong_as_double(rfl64(__double_as_longlong(hv.mn)));
-    const double smx = __longlong_as_double(rfl64(__double_as_longlong(hv.mx)));
+    // with the stats role in this launch, _min/_max are not final yet: markers
+    const double smn = nstat > 0 ? __longlong_as_double(GK_QMARK_MIN)
+                                 : __longlong_as_double(rfl64(__double_as_longlong(hv.mn)));
+    const double smx = nstat > 0 ? __longlong_as_double(GK_QMARK_MAX)
+                                 : __longlong_as_double(rfl64(__double_as_longlong(hv.mx)));
     if (wn < count) gk_hdr_issue(hv, st, offs, list ? (int64_t)list[wn] : wn);
     w = wn;
     if (!list && scls != 0) continue;  // promoted: handled by its class launch
@@ -2761,7 +2895,8 @@ static hipError_t launch_ingest_vpl(int vpl, const GKState& st, const double* x,
 template <int VPL>
 static hipError_t launch_ingest_small(const GKState& st, const double* x, const int64_t* offs, const int32_t* list,
                                       int64_t count, int force, int32_t* ovf_count, int32_t* ovf_list,
-                                      const GKQuery& q, unsigned long long* work, hipStream_t stream) {
+                                      const GKQuery& q, unsigned long long* work, int fused_stats,
+                                      hipStream_t stream) {
   if (count <= 0) return hipSuccess;
   if (!work) return hipErrorInvalidValue;
   int occ = 0;
@@ -2771,10 +2906,21 @@ static hipError_t launch_ingest_small(const GKState& st, const double* x, const 
   int64_t grid = (int64_t)num_cu() * occ;
   if (grid > count) grid = count;
   if (grid < 1) grid = 1;
+  // stats role: fused_stats/4 waves per CU start with the _sum/_avg chains
+  // (only for the batch launch over every stream: x given, no list)
+  int nstat = 0;
+  if (fused_stats > 0 && x && !list) {
+    const int64_t want = std::max<int64_t>(1, (int64_t)num_cu() * fused_stats / 4);  // quarter waves per CU
+    nstat = (int)(grid < want ? grid : want);
+  }
   hipError_t e = hipMemsetAsync(work, 0, GK_WORK_BYTES, stream);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((k_ingest_small<VPL>), dim3((unsigned)grid), dim3(64), 0, stream, st, x, offs, list, count,
-                     force, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode, work);
+                     force, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode, work, nstat);
+  if (nstat > 0 && q.qs && q.nq > 0) {
+    const int64_t tot = st.S * (int64_t)q.nq;
+    hipLaunchKernelGGL(k_qfix, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, st, q.out, q.nq);
+  }
   return hipGetLastError();
 }
 
@@ -2784,11 +2930,13 @@ hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x
                             const int32_t* list, int64_t count, int force, unsigned char* ws, size_t ws_bytes,
                             int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list, const GKQuery& q,
                             unsigned long long* work, const int32_t* prio, const int32_t* prio_count,
-                            const double* psort, const int64_t* prio_ws, hipStream_t stream) {
+                            const double* psort, const int64_t* prio_ws, int fused_stats, hipStream_t stream) {
   switch (cap) {
     case SMALL_CAP:
-      if (vpl == 1) return launch_ingest_small<1>(st, x, offs, list, count, force, ovf_count, ovf_list, q, work, stream);
-      if (vpl == 2) return launch_ingest_small<2>(st, x, offs, list, count, force, ovf_count, ovf_list, q, work, stream);
+      if (vpl == 1)
+        return launch_ingest_small<1>(st, x, offs, list, count, force, ovf_count, ovf_list, q, work, fused_stats, stream);
+      if (vpl == 2)
+        return launch_ingest_small<2>(st, x, offs, list, count, force, ovf_count, ovf_list, q, work, fused_stats, stream);
       return hipErrorInvalidValue;
     case 2048:
       return launch_ingest_vpl<2048>(vpl, st, x, offs, list, count, force, cap, nullptr, 0, 0, ovf_count, ovf_list,
@@ -2801,12 +2949,14 @@ hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x
 }
 
 hipError_t gk_launch_stats(const GKState& st, const double* x, const int64_t* offs, int32_t* long_list,
-                           int64_t* long_n, int32_t* long_count, const GKPresort& ps, hipStream_t stream) {
+                           int64_t* long_n, int32_t* long_count, const GKPresort& ps, int lengths_only,
+                           hipStream_t stream) {
   if (st.S <= 0) return hipSuccess;
   hipError_t e = hipMemsetAsync(long_count, 0, sizeof(int32_t), stream);
   if (e != hipSuccess) return e;
   const int64_t grid = (st.S + 255) / 256;
-  hipLaunchKernelGGL(k_stats, dim3((unsigned)grid), dim3(256), 0, stream, st, x, offs, long_list, long_count);
+  hipLaunchKernelGGL(k_stats, dim3((unsigned)grid), dim3(256), 0, stream, st, x, offs, long_list, long_count,
+                     lengths_only);
   hipLaunchKernelGGL(k_long_prep, dim3(1), dim3(1024), 0, stream, st, offs, long_list, long_n,
                      (const int32_t*)long_count, ps.list_ws, ps.list_b0, ps.ws_cap, ps.ws_need);
   return hipGetLastError();
@@ -2876,6 +3026,17 @@ hipError_t gk_launch_merge(const MergeArgsHost& h, hipStream_t stream) {
   int64_t grid = (int64_t)num_cu() * 8;
   if (grid > h.count) grid = h.count;
   hipLaunchKernelGGL(k_merge<false>, dim3((unsigned)grid), dim3(64), lds, stream, a);
+  return hipGetLastError();
+}
+
+__global__ void k_rtab(GKState st) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < st.rtab_n) st.rtab[k] = k == 0 ? 0.0 : 1.0 / (double)k;  // same IEEE division as gk_stat_step
+}
+
+hipError_t gk_launch_rtab(const GKState& st, hipStream_t stream) {
+  if (!st.rtab || st.rtab_n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rtab, dim3((unsigned)((st.rtab_n + 255) / 256)), dim3(256), 0, stream, st);
   return hipGetLastError();
 }
 

@@ -40,14 +40,17 @@ struct MergeArgsHost {
 
 int gk_num_cu();
 size_t gk_ingest_ws_bytes(int cap, int vpl);
-#define GK_WORK_BYTES 1024  // 8 counters, one 128-byte line each
+#define GK_WORK_BYTES 1152  // 8 hand-out counters + the stats-role batch counter, one 128-byte line each
 // `work`: GK_WORK_BYTES of device counters of the small-class launch (dynamic stream hand-out).
 // cap GK_SMALL_CAP / 2048: LDS kernels; any other cap: global workspace ws (ws_bytes per block, ws_blocks blocks)
 hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x, const int64_t* offs,
                             const int32_t* list, int64_t count, int force, unsigned char* ws, size_t ws_bytes,
                             int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list, const GKQuery& q,
                             unsigned long long* work, const int32_t* prio, const int32_t* prio_count,
-                            const double* psort, const int64_t* prio_ws, hipStream_t stream);
+                            const double* psort, const int64_t* prio_ws, int fused_stats, hipStream_t stream);
+// `fused_stats` > 0: the small-class batch launch (x given, no list) also
+// walks the gk:52-59 stats of every stream of at most GK_STATS_LONG values,
+// in that many waves per CU (then requires the lengths-only k_stats before).
 // `prio` / `prio_count` (device, may be NULL): streams handed out first by the
 // capacity-class kernels (the long streams of the batch, longest first);
 // `psort` / `prio_ws`: their presorted flush batches (GKPresort), or NULL.
@@ -67,7 +70,8 @@ struct GKPresort {
   int64_t* ws_need = nullptr;  // device, 1 value
 };
 hipError_t gk_launch_stats(const GKState& st, const double* x, const int64_t* offs, int32_t* long_list,
-                           int64_t* long_n, int32_t* long_count, const GKPresort& ps, hipStream_t stream);
+                           int64_t* long_n, int32_t* long_count, const GKPresort& ps, int lengths_only,
+                           hipStream_t stream);
 // k_presort over the plan k_long_prep wrote (no-op without a workspace)
 hipError_t gk_launch_presort(const GKState& st, const double* x, const int64_t* offs, const int32_t* long_list,
                              const int64_t* long_n, const int32_t* long_count, const GKPresort& ps,
@@ -80,6 +84,8 @@ hipError_t gk_launch_query_list(const GKState& st, const int32_t* list, const in
 size_t gk_merge_lds_bytes(int cap, int pmax);
 hipError_t gk_launch_merge(const MergeArgsHost& h, hipStream_t stream);
 hipError_t gk_launch_reset(const GKState& st, hipStream_t stream);
+// fills st.rtab (reciprocals 1.0/k, k < st.rtab_n)
+hipError_t gk_launch_rtab(const GKState& st, hipStream_t stream);
 hipError_t gk_launch_export(const GKState& st, const int64_t* offs, double* v, int32_t* g, int32_t* d,
                             hipStream_t stream);
 hipError_t gk_launch_export_pending(const GKState& st, const int64_t* offs, double* v, hipStream_t stream);

@@ -40,6 +40,11 @@ struct GKState {
   int32_t nclass;
 
   double* pbuf;     // pending values: pbuf + s*pmax, insertion order
+
+  // rtab[k] = 1.0/(double)k for 1 <= k < rtab_n (IEEE division, made once on
+  // the device): the gk:54 factor of a wave whose streams share n
+  double* rtab;
+  int64_t rtab_n;
 };
 
 __host__ __device__ inline GKRec* gk_table_ptr(const GKState& st, int64_t s) {

@@ -57,14 +57,18 @@ def test_fast_class_has_no_scratch(resource_report, small_isa):
     per stream (end-of-stream pending copy, the empty-table first flush).
     Keeping them in registers instead (e.g. re-reading the gap info at emit)
     measured 1-2% slower (profiles/r01t_ab_regpressure_REJECTED.txt), so the
-    bound is on the count: a spill inside the flush loops adds many more."""
+    bound is on the count: a spill inside the flush loops adds many more.
+    The stats role (fused_stats_role, run by a few waves before they join the
+    hand-out) adds one more folded value (48 bytes, 11 scratch instructions
+    at most); the ingest-only launch measured the same with and without it
+    (GK_FUSED_STATS=0 rows of profiles/r01z_ab_fused_stats.txt)."""
     fast = {k: v for k, v in resource_report.items() if k.startswith("_Z14k_ingest_small")}
     assert len(fast) == 2
     for k, v in fast.items():
-        assert v.get("ScratchSize [bytes/lane]", 0) <= 32, (k, v)
+        assert v.get("ScratchSize [bytes/lane]", 0) <= 48, (k, v)
     for name, body in small_isa.items():
         ops = re.findall(r"^\s*(scratch_\w+)", body, re.M)
-        assert len(ops) <= 10, (name, ops)
+        assert len(ops) <= 12, (name, ops)
 
 
 def test_no_inline_asm_memory_ops():
