@@ -2374,8 +2374,10 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
 // k_merge: GKArray.merge (gk:111-154) and merge_compress(entries), stream by
 // stream.  The incoming list (self's raw pending values, then the converted
 // records of `other` or the caller's records) is stably ordered by value and
-// the four-rule walk of gk:76-106 runs on lane 0 over LDS: incoming records
-// carry g > 1 here, so the add-path closed form does not apply.
+// the four-rule walk of gk:76-106 runs wave-parallel over LDS: incoming
+// records carry g > 1 here, so the add-path closed form does not apply; each
+// lane re-walks its block of entries from its neighbour's carry until no
+// carry-in changes (k_merge).
 // `other` has already been flushed by the caller (gk:126, gk:137).
 // ===========================================================================
 struct MergeArgs {
