@@ -97,9 +97,9 @@ struct gk_set {
   int32_t* d_tmp_list = nullptr;
   int32_t* d_tmp_slots = nullptr;
   int64_t tmp_alloc = 0;
-  // quarter waves per CU of the small-class batch launch that walk the gk:52-59
+  // eighths of a wave per CU of the small-class batch launch that walk the gk:52-59
   // stats chains first (0: separate k_stats launch); GK_FUSED_STATS overrides
-  int fused_stats = 3;
+  int fused_stats = 7;
   // timing
   bool timing = false;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -433,7 +433,7 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
   h->P = (int)inv + 1;  // gk:60
   h->device = device;
   h->vpl = vpl_for(h->P);
-  if (const char* fs = getenv("GK_FUSED_STATS")) h->fused_stats = std::max(0, std::min(32, atoi(fs)));
+  if (const char* fs = getenv("GK_FUSED_STATS")) h->fused_stats = std::max(0, std::min(64, atoi(fs)));
   GKState& st = h->st;
   st.S = num_streams;
   st.eps = eps;

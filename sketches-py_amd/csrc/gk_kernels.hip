@@ -2054,7 +2054,7 @@ __device__ __attribute__((noinline)) void small_quantiles(SmallLDS<VPL>& L, int 
 // bandwidth idle, while k_stats is a pure stream of the same values; run as a
 // separate launch it cost ~19% of a cfg3 step and cannot share the CUs with
 // the persistent ingest grid (profiles/r01c_ab_concurrent_stats.txt).  So the
-// first `nstat` waves of the small-class launch walk the _sum/_avg chains
+// first `nstat` waves (GK_FUSED_STATS/8 per CU) of the small-class launch walk the _sum/_avg chains
 // first -- 64 streams per wave, one per lane, from a register ring of aligned
 // 16-byte loads (the k_stats_long layout, shallower) -- and then join the
 // ingest hand-out.  Batches of 64 streams are handed out through `swork`.
@@ -2908,11 +2908,11 @@ static hipError_t launch_ingest_small(const GKState& st, const double* x, const 
   int64_t grid = (int64_t)num_cu() * occ;
   if (grid > count) grid = count;
   if (grid < 1) grid = 1;
-  // stats role: fused_stats/4 waves per CU start with the _sum/_avg chains
+  // stats role: fused_stats/8 waves per CU start with the _sum/_avg chains
   // (only for the batch launch over every stream: x given, no list)
   int nstat = 0;
   if (fused_stats > 0 && x && !list) {
-    const int64_t want = std::max<int64_t>(1, (int64_t)num_cu() * fused_stats / 4);  // quarter waves per CU
+    const int64_t want = std::max<int64_t>(1, (int64_t)num_cu() * fused_stats / 8);  // eighths of a wave per CU
     nstat = (int)(grid < want ? grid : want);
   }
   hipError_t e = hipMemsetAsync(work, 0, GK_WORK_BYTES, stream);
