@@ -380,6 +380,32 @@ def test_fused_ingest_quantiles_vs_oracle(gpu_device):
             assert_same_state(ss, osx, "fused state eps=%g" % eps)
 
 
+@pytest.mark.parametrize("fused", ["0", "1", "64"])
+def test_stats_role_sizes_vs_oracle(gpu_device, monkeypatch, fused):
+    """The gk:52-59 stats in every layout of the small-class launch: a
+    separate k_stats launch (GK_FUSED_STATS=0), one stats wave (1/8 per CU:
+    the stats finish last), every resident wave (64).  Mixed histories (n
+    differs inside a 64-stream batch: per-lane reciprocals) and fresh batches
+    (shared n: the reciprocal table), streams past GK_STATS_LONG (k_stats_long),
+    and fused quantiles that are _min/_max (k_qfix markers)."""
+    monkeypatch.setenv("GK_FUSED_STATS", fused)
+    rng = np.random.default_rng(47)
+    eps, S = 0.01, 900
+    ss = _ss(S, eps, gpu_device)
+    osx = OracleSet(S, eps)
+    for part in range(3):
+        lens = rng.integers(0, 2500, S) if part else np.full(S, 1000)
+        if part == 2:
+            lens[::97] = 20000
+        seqs = [gen(int(d), int(L), rng) for d, L in zip(rng.integers(0, 8, S), lens)]
+        flat, offs = csr(seqs)
+        qs = [0.0, 0.5, 0.99, 1.0]
+        got = ss.ingest(torch.from_numpy(flat), torch.from_numpy(offs), quantiles=qs)
+        osx.ingest(flat, offs)
+        assert_same_quantiles(got.cpu().numpy(), osx.quantiles(qs), "stats role %s part %d" % (fused, part))
+        assert_same_state(ss, osx, "stats role %s part %d" % (fused, part))
+
+
 def test_long_stream_stats(gpu_device):
     """Streams longer than GK_STATS_LONG (16384) take k_stats_long: _sum/_avg
     chain and first-occurrence _min/_max (signed zeros) across calls."""
