@@ -51,8 +51,10 @@ def main(d, n_values, streams):
     w_ing = avg_of(write, wnames, ing)
     f_st = avg_of(fetch, fnames, "k_stats(")  # not k_stats_long (empty launches in cfg3)
     cal = None
-    if f_st:
-        stats_alg = 8.0 * n_values + 8.0 * (streams + 1) + 40.0 * streams
+    stats_alg = 8.0 * n_values + 8.0 * (streams + 1) + 40.0 * streams
+    # only meaningful while k_stats reads the values (with the stats role in
+    # the small-class launch it only reads the offsets: no calibration)
+    if f_st and f_st * 1024.0 > 0.1 * stats_alg:
         cal = stats_alg / (f_st * 1024.0)
     out["k_ingest"] = {"fetch_bytes_raw": f_ing * 1024 if f_ing else None,
                        "write_bytes": w_ing * 1024 if w_ing else None,
