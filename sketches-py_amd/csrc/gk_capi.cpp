@@ -366,12 +366,15 @@ int run_merge(gk_set* dst, const MergeArgsHost& base, hipStream_t s) {
   a.ovf_count = dst->d_ovf_count;
   a.ovf_list = dst->d_ovf_list;
   std::vector<int32_t> todo;
+  // host source of promote()'s async copies: outlives them (the next
+  // read_overflow synchronises the stream), like gk_import's `by`
+  std::vector<int32_t> up;
   for (int level = 0; level < dst->st.nclass; ++level) {
     const int cap = dst->st.cap[level];
     if (level > 0 && todo.empty()) break;
     if (level > 0) {
       // streams below this class are promoted so that their output may grow
-      std::vector<int32_t> up;
+      up.clear();
       for (int32_t id : todo)
         if (dst->h_cls[id] < level) up.push_back(id);
       int rc = promote(dst, up, level, s);
@@ -475,6 +478,7 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
   okm &= hipMalloc(&st.pbuf, (size_t)S * st.pmax * sizeof(double)) == hipSuccess;
   st.rtab_n = kRecipTable;
   okm &= hipMalloc(&st.rtab, (size_t)st.rtab_n * sizeof(double)) == hipSuccess;
+  okm &= hipMalloc(&st.n0, S * sizeof(int64_t)) == hipSuccess;
   okm &= hipMalloc(&h->d_ovf, (S + 1) * sizeof(int32_t)) == hipSuccess;
   okm &= hipHostMalloc(&h->h_ovf, (std::min<int64_t>(S, kOvfPrefix) + 1) * sizeof(int32_t)) == hipSuccess;
   h->d_ovf_count = h->d_ovf;
@@ -525,7 +529,7 @@ int gk_destroy(gk_set* h) {
                   st.pbuf,    h->d_list[0],   h->d_list[1],     h->d_list[2],   h->d_qs,       h->d_ovf,
                   h->d_tmp_list, h->d_tmp_slots, h->d_ws, h->d_zero_offs, h->d_work,
                   h->d_long_list, h->d_long_n, h->d_long_count, h->ps.list_ws, h->ps.list_b0, h->ps.ws,
-                  h->ps.ws_need, st.rtab};
+                  h->ps.ws_need, st.rtab, st.n0};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (auto& e : h->ev)

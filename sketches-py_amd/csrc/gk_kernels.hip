@@ -248,7 +248,12 @@ __global__ __launch_bounds__(256) void k_stats(GKState st, const double* __restr
   }
   __syncthreads();
   int64_t L = 0;
-  if (t < nstr) L = so[t + 1] - so[t];
+  if (t < nstr) {
+    L = so[t + 1] - so[t];
+    // pre-call n for the stats role of the small-class launch that follows
+    // (its ingest waves rewrite st.n[s] while the role still walks stream s)
+    st.n0[s0 + t] = st.n[s0 + t];
+  }
   if (L > GK_STATS_LONG) {  // walked by k_stats_long, not in this block's trip count
     long_list[atomicAdd(long_count, 1)] = (int32_t)(s0 + t);
     L = 0;
@@ -2072,7 +2077,9 @@ __device__ __forceinline__ void fused_stats_role(const GKState& st, const double
                                                  const int64_t* __restrict__ offs,
                                                  unsigned long long* __restrict__ swork, int lane) {
   const int64_t nb = (st.S + 63) / 64;
-  const double2* __restrict__ dummy = (const double2*)(x + ((((uintptr_t)x) & 8) ? 1 : 0));
+  // refills past a lane's last chunk read this instead (st.rtab: 1 MiB the set
+  // owns, 16-byte aligned; the values are never used)
+  const double2* __restrict__ dummy = (const double2*)st.rtab;
   for (;;) {
     unsigned long long v = 0;
     if (lane == 0) v = atomicAdd(swork, 1ull);
@@ -2087,7 +2094,7 @@ __device__ __forceinline__ void fused_stats_role(const GKState& st, const double
     int64_t n = 0;
     double mn = 0, mx = 0, sm = 0, av = 0;
     if (act) {
-      n = st.n[s];
+      n = st.n0[s];  // pre-call n (k_stats snapshot): st.n[s] may already be the ingest's
       mn = st.mn[s];
       mx = st.mx[s];
       sm = st.sum[s];

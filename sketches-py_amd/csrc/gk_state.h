@@ -45,6 +45,11 @@ struct GKState {
   // the device): the gk:54 factor of a wave whose streams share n
   double* rtab;
   int64_t rtab_n;
+
+  // pre-call n of every stream, written by k_stats before an ingest launch:
+  // the stats role of k_ingest_small reads it while ingest waves of the same
+  // launch rewrite n (scratch, S entries)
+  int64_t* n0;
 };
 
 __host__ __device__ inline GKRec* gk_table_ptr(const GKState& st, int64_t s) {

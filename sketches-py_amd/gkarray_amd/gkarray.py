@@ -203,12 +203,19 @@ class GKArray:
             out = self._set.quantiles(safe, single=True)[0].cpu().tolist() if qs else []
             return [np.nan if k in nan_pos else np.float64(v) for k, v in enumerate(out)]
         if isinstance(q_values, np.ndarray):
-            # gk:205: `ndarray != list` is an array; its truth value raises
-            raise ValueError("The truth value of an array with more than one element is ambiguous. "
-                             "Use a.any() or a.all()")
+            # gk:205: `ndarray != list` is an elementwise array; numpy's truth
+            # value of it raises unless it has exactly one element
+            if q_values.size == 0:
+                raise ValueError("The truth value of an empty array is ambiguous. "
+                                 "Use `array.size > 0` to check that an array is not empty.")
+            if q_values.size > 1:
+                raise ValueError("The truth value of an array with more than one element is ambiguous. "
+                                 "Use a.any() or a.all()")
+            single = bool(nan_pos)  # [nan] != [nan]: per-q quantile(), which raises below
+        else:
+            # gk:205: a tuple never equals sorted(...) (a list) -> per-q quantile()
+            single = (not isinstance(q_values, list)) or (qs != sorted(qs))
         if nan_pos:
             raise ValueError("cannot convert float NaN to integer")
-        # gk:205: a tuple never equals sorted(...) (a list) -> per-q quantile()
-        single = (not isinstance(q_values, list)) or (qs != sorted(qs))
         out = self._set.quantiles([float(q) for q in qs], single=single)[0].cpu().tolist()
         return [np.nan if math.isnan(v) else v for v in out]

@@ -1,0 +1,101 @@
+"""Shared helpers of the GPU parity tests (HIP path through the C ABI vs the
+oracle / the golden vectors).  Test infrastructure only."""
+import numpy as np
+import torch
+
+import golden_io as G
+from gk_oracle_c import OracleSet  # noqa: F401  (re-exported for the tests)
+
+
+def _ss(S, eps, dev, **kw):
+    from gkarray_amd import StreamSet
+    return StreamSet(S, eps, device=dev, **kw)
+
+
+def same_q(a, b, small):
+    # signed-zero tolerance only for the small-n percentile branch (gk:169-171, 200-202)
+    return G.same_float(a, b) or (bool(small) and a == 0 and b == 0)
+
+
+def small_n(n, eps):
+    """Per-stream flag of the small-n branch: n < 1/eps (gk:169 / gk:200)."""
+    return np.asarray(n, dtype=np.float64) < 1.0 / eps
+
+
+def small_of(osx, eps):
+    return small_n(osx.stats()["n"], eps)
+
+
+def csr(seqs):
+    offs = np.zeros(len(seqs) + 1, np.int64)
+    offs[1:] = np.cumsum([len(x) for x in seqs])
+    flat = np.concatenate([np.asarray(x, np.float64) for x in seqs]) if len(seqs) else np.zeros(0)
+    return flat, offs
+
+
+def ingest_np(ss, seqs):
+    flat, offs = csr(seqs)
+    ss.ingest(torch.from_numpy(flat), torch.from_numpy(offs))
+
+
+def tables_np(ss):
+    offs, v, g, d = ss.tables()
+    return offs.cpu().numpy(), v.cpu().numpy(), g.cpu().numpy(), d.cpu().numpy()
+
+
+def assert_same_tables(ss, osx, ids=None, what=""):
+    go, gv, gg, gd = tables_np(ss)
+    oo, ov, og, od = osx.tables()
+    S = ss.num_streams
+    ids = range(S) if ids is None else ids
+    for s in ids:
+        a, b = go[s], go[s + 1]
+        c, e = oo[s], oo[s + 1]
+        assert b - a == e - c, "%s stream %d: size %d vs %d" % (what, s, b - a, e - c)
+        assert np.array_equal(gv[a:b].view(np.int64), ov[c:e].view(np.int64)), "%s stream %d values" % (what, s)
+        assert np.array_equal(gg[a:b].astype(np.int64), og[c:e]), "%s stream %d g" % (what, s)
+        assert np.array_equal(gd[a:b].astype(np.int64), od[c:e]), "%s stream %d delta" % (what, s)
+
+
+def assert_same_state(ss, osx, what=""):
+    assert_same_tables(ss, osx, what=what)
+    gp_o, gp_v = ss.pending()
+    op_o, op_v = osx.pending()
+    assert np.array_equal(gp_o.cpu().numpy(), op_o), what + " pending offsets"
+    assert np.array_equal(gp_v.cpu().numpy().view(np.int64), op_v.view(np.int64)), what + " pending"
+    st = {k: v.cpu().numpy() for k, v in ss.stats().items()}
+    ost = osx.stats()
+    for k in ("n", "size", "pending"):
+        assert np.array_equal(st[k].astype(np.int64), ost[k].astype(np.int64)), what + " " + k
+    for k in ("min", "max", "sum", "avg"):
+        assert np.array_equal(st[k].view(np.int64), ost[k].view(np.int64)), what + " " + k
+
+
+def assert_same_quantiles(got, exp, what, small):
+    """got/exp: [S, nq] (small: per-stream flags [S]) or [nq] (small: scalar)."""
+    got = np.asarray(got)
+    exp = np.asarray(exp)
+    assert got.shape == exp.shape
+    sm = np.broadcast_to(np.asarray(small, dtype=bool).reshape(-1, *([1] * (got.ndim - 1)))
+                         if got.ndim > 1 else np.asarray(small, dtype=bool), got.shape)
+    bad = [(i, got.flat[i], exp.flat[i]) for i in range(got.size)
+           if not same_q(got.flat[i], exp.flat[i], sm.flat[i])]
+    assert not bad, "%s: %d mismatches, first %r" % (what, len(bad), bad[:3])
+
+
+def gen(dist, L, rng):
+    if dist == 0:
+        return rng.random(L)
+    if dist == 1:
+        return rng.lognormal(0, 1, L)
+    if dist == 2:
+        return rng.pareto(1.5, L) + 1
+    if dist == 3:
+        return np.sort(rng.random(L))[::-1].copy()
+    if dist == 4:
+        return np.sort(rng.random(L))
+    if dist == 5:
+        return rng.integers(0, 5, L).astype(np.float64)
+    if dist == 6:
+        return rng.choice(np.array([0.0, -0.0, 1.0, -1.0]), L)
+    return np.round(rng.normal(0, 2, L), 1)
