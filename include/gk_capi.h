@@ -14,12 +14,20 @@
  *  - Pointers documented "device" must be device memory on the set's GPU
  *    (e.g. a torch tensor's data_ptr()); "host" pointers are host memory.
  *  - `stream` is a hipStream_t passed as void* (NULL = the default stream).
- *    Work is enqueued on it; calls that return host-visible scalars
- *    (counts, errors) synchronise it before returning.  gk_ingest /
- *    gk_ingest_quantiles may run part of their work (the sequential
- *    _sum/_avg chains of streams longer than 16384 values) on a stream the
- *    set owns; `stream` waits for it before the call returns, so every later
- *    call enqueued on `stream` sees the finished state.
+ *    All calls on one set must be ordered on one stream.  gk_ingest,
+ *    gk_ingest_quantiles, gk_flush, gk_quantiles, gk_stats and the exports
+ *    only ENQUEUE their work and return (no host synchronisation): a stream
+ *    whose table outgrows its capacity class is moved to the next class and
+ *    re-run by the device itself.  Part of an ingest (the sequential
+ *    _sum/_avg chains of streams longer than 16384 values) runs on a stream
+ *    the set owns; `stream` is made to wait for it, so every later call
+ *    enqueued on `stream` sees the finished state.  The caller keeps input
+ *    buffers alive until that work has run (stream order).  gk_merge,
+ *    gk_merge_compress, gk_import, gk_save / gk_load and gk_num_promoted
+ *    synchronise before returning.
+ *  - Asynchronous errors: a stream that outgrows even the largest class (or
+ *    finds no free slot in it) keeps its previous state and is reported as
+ *    GK_E_OVERFLOW by a later call on the set, at the latest by gk_sync.
  *  - A set is not thread-safe.  The library owns the set's device state;
  *    callers own their input and output buffers.
  */
@@ -39,6 +47,8 @@ extern "C" {
 #define GK_E_HIP (-4)          /* HIP runtime failure                              */
 #define GK_E_NOMEM (-5)        /* device allocation failed                          */
 #define GK_E_UNSUPPORTED (-6)  /* eps outside the supported range                  */
+#define GK_E_IO (-7)           /* state file cannot be opened / written            */
+#define GK_E_FORMAT (-8)       /* state file malformed, wrong version or checksum  */
 
 typedef struct gk_set gk_set;
 
@@ -67,6 +77,10 @@ int gk_reset(gk_set* set, void* stream);
  * happen at exactly the reference's flush points (n % (int(1/eps)+1) == 0). */
 int gk_ingest(gk_set* set, const double* values, const int64_t* offsets,
               void* stream);
+
+/* Wait for the set's work on `stream`; return (and clear) an asynchronous
+ * error of an earlier call (GK_E_OVERFLOW, see Conventions) or GK_OK. */
+int gk_sync(gk_set* set, void* stream);
 
 /* GKArray.merge_compress() with no argument (gk:63-109) on every stream that
  * has pending values -- what size()/quantile()/quantiles() do first
@@ -132,6 +146,22 @@ int gk_import(gk_set* set, const int64_t* offs, const double* v,
               const double* pv, const int64_t* n, const double* mn,
               const double* mx, const double* sum, const double* avg,
               void* stream);
+
+/* Versioned state files (format: sketches-py_amd/csrc/gk_format.h, "GKSTATE"
+ * version 1: header with magic, version, eps, S, record totals and a
+ * checksum; then sizes, pending counts, n/min/max/sum/avg, the tables and the
+ * pending values).  The reference has no serialization: its state is the
+ * Python object (gk:21-29 -- entries, incoming, _n, _min, _max, _sum, _avg),
+ * and this is that state per stream, saved WITHOUT flushing, so a set loaded
+ * from a file continues exactly like the saved one.
+ * gk_save writes the set's state to `path`.  gk_peek reads eps and the stream
+ * count from a file's header (to create a matching set).  gk_load replaces
+ * the state of every stream of `set`, which must have the file's stream count
+ * (GK_E_ARG) and eps (GK_E_EPS_MISMATCH).  GK_E_IO / GK_E_FORMAT on
+ * unreadable, malformed, wrong-version or corrupt files. */
+int gk_save(gk_set* set, const char* path, void* stream);
+int gk_peek(const char* path, double* eps, int64_t* num_streams);
+int gk_load(gk_set* set, const char* path, void* stream);
 
 /* Introspection for tests and benchmarks. */
 int64_t gk_num_streams(const gk_set* set);

@@ -1,0 +1,38 @@
+/*
+ * gk_cpu.h -- the host (CPU) engine of the batched GKArray.
+ *
+ * libgkarray_cpu.so (sketches-py_amd/cpu/gk_cpu.cpp) implements EVERY entry
+ * point of gk_capi.h with the same names, arguments, status codes and
+ * semantics, on host memory:
+ *  - every pointer documented "device" in gk_capi.h is a HOST pointer here;
+ *  - `stream` arguments are ignored (all calls are synchronous, gk_sync is a
+ *    no-op), `device` of gk_create is ignored;
+ *  - there are no capacity classes: tables and pending buffers grow without
+ *    bound, any eps in (0, 1] is accepted, GK_E_OVERFLOW never occurs;
+ *  - streams are processed in parallel on host threads (each stream strictly
+ *    in insertion order): GK_CPU_THREADS (environment) or gk_cpu_set_threads,
+ *    default = the CPUs this process may run on.
+ * It is selected explicitly (Python: StreamSet(..., device="cpu")); the HIP
+ * library never falls back to it.  Results are bit-identical to the HIP
+ * engine and to gkarray.py (reference gk:19-232).
+ */
+#ifndef GK_CPU_H
+#define GK_CPU_H
+
+#include "gk_capi.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Host threads used by later calls on `set` (0 = the default). */
+int gk_cpu_set_threads(gk_set* set, int threads);
+
+/* Host threads the set currently uses. */
+int gk_cpu_threads(const gk_set* set);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GK_CPU_H */

@@ -1,11 +1,15 @@
-# GPU check after a kernel change: -m gpu parity tests, then cfg3 / cfg2 bench lines (no CPU leg).
+# Round check on the GPU box: -m gpu tests (parity, configs, state files),
+# smoke, default bench line, kernel trace of the bench.  Usage: gpu_check.sh TAG
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 TAG=${1:-chk}
-timeout -k 10 900 python -m pytest tests -m gpu -q -x > gpurun_out/${TAG}_pytest.log 2>&1
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/${TAG}_pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/${TAG}_pytest.log
-if [ $rc -ne 0 ]; then tail -60 gpurun_out/${TAG}_pytest.log | cut -c1-300; exit 1; fi
-for wl in cfg3 cfg2; do
-  timeout -k 10 300 python bench.py --workload $wl --no-cpu --steps 5 --warmup 2 > gpurun_out/${TAG}_$wl.log 2>&1 || exit $?
-  grep '^{"metric"' gpurun_out/${TAG}_$wl.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('$wl', 'Gv/s=%.2f'%(d['value']/1e9), 'ms/step=%.2f'%d['ms_per_step'], 'ingest_ms=%.2f'%r['launch_ms'], 'stats_ms=%.2f'%r['stats_kernel_ms'], 'GB/s=%.0f'%r['achieved'])"
-done
+if [ $rc -ne 0 ]; then grep -E "FAILED|Error|error" gpurun_out/${TAG}_pytest.log | head -20; tail -40 gpurun_out/${TAG}_pytest.log | cut -c1-300; exit 1; fi
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || exit $?
+tail -1 gpurun_out/${TAG}_smoke.log
+timeout -k 10 400 python bench.py > gpurun_out/${TAG}_bench.log 2>&1 || exit $?
+tail -1 gpurun_out/${TAG}_bench.log | cut -c1-600
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_trace -o run -- \
+  python3 bench.py --no-cpu --steps 5 --warmup 2 > gpurun_out/${TAG}_trace.log 2>&1 || exit $?
+tail -1 gpurun_out/${TAG}_trace.log | cut -c1-300

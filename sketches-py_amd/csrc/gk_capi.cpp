@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "gk_capi.h"
+#include "gk_format.h"
 #include "gk_launch.h"
 #include "gk_state.h"
 
@@ -40,11 +41,11 @@ int fail(int code, const char* fmt, ...) {
   } while (0)
 
 constexpr int kCapSmall = GK_SMALL_CAP;  // LDS class (gk_launch.h)
-constexpr int64_t kOvfPrefix = 4096;     // overflow entries read back with the count
 constexpr int kCapLarge = 2048;  // LDS class, ~92 KB per wave
 constexpr int kCapHuge = 32768;  // global-workspace class
 constexpr int64_t kRecipTable = (int64_t)1 << 17;  // entries of st.rtab (1 MiB)
 constexpr int kMaxLdsCap = 2048;
+constexpr int kRounds = GK_MAX_CLASSES + 1;  // overflow lists: launch round 0 + one per promotion level
 
 int vpl_for(int P) {
   int v = 1;
@@ -61,23 +62,37 @@ struct gk_set {
   int device = 0;
   int vpl = 1;
   GKState st{};
-  std::vector<int8_t> h_cls;  // host mirror of st.cls
-  // per class c >= 1: arena bookkeeping and member list (host + device copy)
-  int64_t slots_alloc[GK_MAX_CLASSES] = {0, 0, 0};
-  int64_t slots_used[GK_MAX_CLASSES] = {0, 0, 0};
-  std::vector<int32_t> members[GK_MAX_CLASSES];
+  // Capacity classes c > 0 live entirely on the device: slot counters, member
+  // lists and re-run lists (GKPoolDev, k_promote_dev).  The host only sizes
+  // the arenas (st.alloc) ahead of need, from counters read back
+  // asynchronously at the end of each call (h_ctr, ev_done).
+  int32_t* d_ctr = nullptr;                                  // GK_CTR_WORDS counters
   int32_t* d_list[GK_MAX_CLASSES] = {nullptr, nullptr, nullptr};
-  int64_t list_alloc[GK_MAX_CLASSES] = {0, 0, 0};
+  int32_t* d_rerun[GK_MAX_CLASSES] = {nullptr, nullptr, nullptr};
+  int32_t* d_defer = nullptr;  // streams whose next class had no free slot (S entries)
+  int32_t* h_ctr = nullptr;  // pinned: the counters as of the end of the last call
+  hipEvent_t ev_done = nullptr;
+  bool done_pending = false;
+  // the last ingest / flush call: its inputs, kept to re-run deferred streams
+  // (the caller keeps them valid until the set's next call or gk_sync)
+  struct {
+    const double* x = nullptr;
+    const int64_t* offs = nullptr;
+    int force = 0;
+    GKQuery q;
+    bool may_defer = false;  // some class could run out of slots in it
+  } last;
+  int32_t fatal_seen = 0;  // device FATAL count already reported
+  int sticky = GK_OK;      // asynchronous error reported by the next call / gk_sync
+  std::string sticky_msg;
   // global workspace for classes beyond LDS
   unsigned char* d_ws = nullptr;
   size_t ws_bytes = 0;
   int64_t ws_blocks = 0;
-  // overflow reporting
-  int32_t* d_ovf_count = nullptr;  // d_ovf[0]
-  int32_t* d_ovf_list = nullptr;   // d_ovf + 1: one buffer, so count + list come back in one copy
-  int32_t* d_ovf = nullptr;
-  int32_t* h_ovf = nullptr;        // pinned: count + the first kOvfPrefix list entries
-  std::vector<int32_t> h_slots[GK_MAX_CLASSES];  // promotion slots per target class (kept until the next sync)
+  // overflow lists of the launch rounds (device); counts in one array
+  int32_t* d_ovfc = nullptr;              // kRounds counts
+  int32_t* d_ovfl[kRounds] = {nullptr, nullptr, nullptr, nullptr};
+  int32_t* h_ovf = nullptr;               // pinned readback of a count (+ list) for merge / import
   int64_t* d_zero_offs = nullptr;  // S+1 zeros: offsets of flush-only launches
   unsigned long long* d_work = nullptr;  // stream hand-out counter of the small-class kernel
   int32_t* d_long_list = nullptr;        // streams k_stats hands to k_stats_long (longest first)
@@ -90,37 +105,32 @@ struct gk_set {
   // presorted flush batches of long streams (sets whose class 0 is the 2048
   // class): plan arrays, workspace, and the size the last call needed
   GKPresort ps;
-  int64_t* h_ws_need = nullptr;  // pinned host copy of *ps.ws_need
-  // scratch
+  int64_t* h_ws_need = nullptr;  // pinned host copy of *ps.ws_need (valid once ev_done completed)
+  // query scratch: pinned host copy of qs (the async H2D reads it), device copy
+  double* h_qs = nullptr;
   double* d_qs = nullptr;
   int qs_alloc = 0;
-  int32_t* d_tmp_list = nullptr;
-  int32_t* d_tmp_slots = nullptr;
-  int64_t tmp_alloc = 0;
+  hipEvent_t ev_qs = nullptr;  // the last H2D copy out of h_qs
   // eighths of a wave per CU of the small-class batch launch that walk the gk:52-59
   // stats chains first (0: separate k_stats launch); GK_FUSED_STATS overrides
   int fused_stats = 7;
-  // timing
+  // timing: event pairs recorded around the timed launches, summed at read
   bool timing = false;
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  double flush_ms = 0, stats_ms = 0;
-  int64_t launches = 0;
+  std::vector<hipEvent_t> tev_flush, tev_stats;
+  size_t n_flush = 0, n_stats = 0;
 };
 
 namespace {
 
-int ensure_tmp(gk_set* h, int64_t n) {
-  if (n <= h->tmp_alloc) return GK_OK;
-  if (h->d_tmp_list) (void)hipFree(h->d_tmp_list);
-  if (h->d_tmp_slots) (void)hipFree(h->d_tmp_slots);
-  h->d_tmp_list = nullptr;
-  h->d_tmp_slots = nullptr;
-  const int64_t cap = std::max<int64_t>(n, 1024);
-  if (hipMalloc(&h->d_tmp_list, cap * sizeof(int32_t)) != hipSuccess ||
-      hipMalloc(&h->d_tmp_slots, cap * sizeof(int32_t)) != hipSuccess)
-    return fail(GK_E_NOMEM, "scratch allocation of %lld entries failed", (long long)cap);
-  h->tmp_alloc = cap;
-  return GK_OK;
+GKPoolDev pool_args(const gk_set* h) {
+  GKPoolDev p;
+  p.ctr = h->d_ctr;
+  p.defer = h->d_defer;
+  for (int c = 0; c < GK_MAX_CLASSES; ++c) {
+    p.list[c] = h->d_list[c];
+    p.rerun[c] = h->d_rerun[c];
+  }
+  return p;
 }
 
 int ensure_ws(gk_set* h) {
@@ -129,7 +139,10 @@ int ensure_ws(gk_set* h) {
   if (cap <= kMaxLdsCap) return GK_OK;
   size_t b = std::max(gk_ingest_ws_bytes(cap, h->vpl), gk_merge_lds_bytes(cap, h->st.pmax));
   b = (b + 4095) & ~(size_t)4095;
-  int64_t blocks = std::min<int64_t>(gk_num_cu(), 256);
+  // blocks of the global-workspace class: it only holds the rare streams
+  // whose tables outgrow LDS, so a few blocks per 4096 streams
+  int64_t blocks = std::min<int64_t>(gk_num_cu(), std::max<int64_t>(8, h->S / 4096));
+  if (h->st.cap[0] > kMaxLdsCap) blocks = std::min<int64_t>(gk_num_cu(), 256);  // every stream is there
   if (hipMalloc(&h->d_ws, b * blocks) != hipSuccess)
     return fail(GK_E_NOMEM, "workspace of %lld x %zu bytes failed", (long long)blocks, b);
   h->ws_bytes = b;
@@ -137,100 +150,162 @@ int ensure_ws(gk_set* h) {
   return GK_OK;
 }
 
-// Grow the arena of class c so that `need` slots exist (copying live slots).
-int ensure_slots(gk_set* h, int c, int64_t need, hipStream_t stream) {
-  if (need <= h->slots_alloc[c]) return GK_OK;
-  int64_t cap = std::max<int64_t>(h->slots_alloc[c] * 2, std::max<int64_t>(need, c == 1 ? 256 : 16));
+// Slots a class starts with (grown on demand, see grow_pools): every stream
+// while that costs at most 1 GiB (then no call can run out of slots), else a
+// share of the streams.
+int64_t initial_slots(const gk_set* h, int c) {
+  const int64_t S = std::max<int64_t>(h->S, 1);
+  if (const char* e = getenv("GK_POOL_SLOTS"))  // tests: force tiny arenas (deferral / growth paths)
+    return std::max<int64_t>(1, std::min<int64_t>(S, atoll(e)));
+  const int64_t slot_bytes = (int64_t)h->st.cap[c] * (int64_t)sizeof(GKRec);
+  if (S * slot_bytes <= ((int64_t)1 << 30)) return S;
+  const int64_t n = h->st.cap[c] <= kCapLarge ? std::max<int64_t>(4096, S / 16) : std::max<int64_t>(64, S / 1024);
+  return std::min<int64_t>(n, S);
+}
+
+// Grow class c's arena to `want` slots, keeping the slots handed out so far.
+// Synchronises `s` (the arena may be in use by earlier launches).
+int grow_class(gk_set* h, int c, int64_t want, hipStream_t s) {
+  want = std::min<int64_t>(want, std::max<int64_t>(h->S, 1));
+  if (want <= h->st.alloc[c]) return GK_OK;
+  HIP_TRY(hipStreamSynchronize(s));
+  int32_t used = 0;
+  HIP_TRY(hipMemcpy(&used, h->d_ctr + GK_CTR_USED + c, sizeof(int32_t), hipMemcpyDeviceToHost));
+  const int64_t keep = std::min<int64_t>(std::max(used, 0), h->st.alloc[c]);
   GKRec* nt = nullptr;
-  if (hipMalloc(&nt, (size_t)cap * h->st.cap[c] * sizeof(GKRec)) != hipSuccess)
-    return fail(GK_E_NOMEM, "class-%d arena of %lld slots failed", c, (long long)cap);
-  if (h->st.tab[c]) {
-    HIP_TRY(hipMemcpyAsync(nt, h->st.tab[c], (size_t)h->slots_used[c] * h->st.cap[c] * sizeof(GKRec),
-                           hipMemcpyDeviceToDevice, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
-    (void)hipFree(h->st.tab[c]);
+  if (hipMalloc(&nt, (size_t)want * h->st.cap[c] * sizeof(GKRec)) != hipSuccess)
+    return fail(GK_E_NOMEM, "class-%d arena of %lld slots failed", c, (long long)want);
+  if (h->st.tab[c] && keep) {
+    HIP_TRY(hipMemcpy(nt, h->st.tab[c], (size_t)keep * h->st.cap[c] * sizeof(GKRec), hipMemcpyDeviceToDevice));
   }
+  if (h->st.tab[c]) (void)hipFree(h->st.tab[c]);
   h->st.tab[c] = nt;
-  h->slots_alloc[c] = cap;
+  h->st.alloc[c] = (int32_t)want;
   return GK_OK;
 }
 
-int sync_list(gk_set* h, int c, hipStream_t stream) {
-  const int64_t n = (int64_t)h->members[c].size();
-  if (n > h->list_alloc[c]) {
-    if (h->d_list[c]) (void)hipFree(h->d_list[c]);
-    h->d_list[c] = nullptr;
-    const int64_t cap = std::max<int64_t>(n * 2, 256);
-    if (hipMalloc(&h->d_list[c], cap * sizeof(int32_t)) != hipSuccess)
-      return fail(GK_E_NOMEM, "class-%d list allocation failed", c);
-    h->list_alloc[c] = cap;
+// Consume the counters read back at the end of the last call: report streams
+// that found no class / slot (sticky GK_E_OVERFLOW), learn the presort
+// workspace the last call needed.  block: wait for that call to finish.
+void poll(gk_set* h, bool block) {
+  if (!h->done_pending) return;
+  if (block) {
+    if (hipEventSynchronize(h->ev_done) != hipSuccess) return;
+  } else if (hipEventQuery(h->ev_done) != hipSuccess) {
+    return;
   }
-  if (n)
-    HIP_TRY(hipMemcpyAsync(h->d_list[c], h->members[c].data(), n * sizeof(int32_t), hipMemcpyHostToDevice, stream));
+  h->done_pending = false;
+  const int32_t fatal = h->h_ctr[GK_CTR_FATAL];
+  if (fatal > h->fatal_seen && h->sticky == GK_OK) {
+    char buf[256];
+    snprintf(buf, sizeof(buf),
+             "%d stream(s) (largest id %d) outgrew every table capacity class (largest %d entries) or found no "
+             "free slot: their values of that call were not added",
+             fatal - h->fatal_seen, h->h_ctr[GK_CTR_FATAL + 1], h->st.cap[h->st.nclass - 1]);
+    h->sticky = GK_E_OVERFLOW;
+    h->sticky_msg = buf;
+  }
+  h->fatal_seen = fatal;
+}
+
+int promote_rounds(gk_set* h, const double* x, const int64_t* offs, int force, const GKQuery& q, hipStream_t s);
+int mark_done(gk_set* h, hipStream_t s);
+
+// Streams the last call deferred (their next class had no free slot): grow
+// the arenas and run them again, from that call's inputs, before anything
+// else touches the set.
+int replay_deferred(gk_set* h, hipStream_t s) {
+  for (int guard = 0; guard < 8; ++guard) {
+    const int32_t nd = h->h_ctr[GK_CTR_DEFER];
+    if (nd <= 0) return GK_OK;
+    h->h_ctr[GK_CTR_DEFER] = 0;
+    for (int c = 1; c < h->st.nclass; ++c) {
+      const int64_t used = h->h_ctr[GK_CTR_USED + c];
+      int rc = grow_class(h, c, std::max<int64_t>(2 * (int64_t)h->st.alloc[c], used + 2 * (int64_t)nd), s);
+      if (rc) return rc;
+    }
+    // the deferred list becomes round 0's overflow list
+    HIP_TRY(hipMemsetAsync(h->d_ovfc, 0, kRounds * sizeof(int32_t), s));
+    HIP_TRY(hipMemcpyAsync(h->d_ovfl[0], h->d_defer, (size_t)nd * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+    HIP_TRY(hipMemcpyAsync(h->d_ovfc, h->d_ctr + GK_CTR_DEFER, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+    HIP_TRY(hipMemsetAsync(h->d_ctr + GK_CTR_DEFER, 0, sizeof(int32_t), s));
+    int rc = promote_rounds(h, h->last.x, h->last.offs, h->last.force, h->last.q, s);
+    if (!rc) rc = mark_done(h, s);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(s));
+    poll(h, true);
+  }
+  return fail(GK_E_OVERFLOW, "deferred streams could not be placed in a capacity class");
+}
+
+// Before a call (and in gk_sync): settle the previous call -- wait for it when
+// it may have deferred streams (some class could run out of slots), re-run
+// those, report its asynchronous errors.
+int settle(gk_set* h, hipStream_t s, bool block) {
+  poll(h, block || h->last.may_defer);
+  if (h->done_pending) return GK_OK;  // still running, and it cannot have deferred anything
+  return replay_deferred(h, s);
+}
+
+// Before a call: keep every class's arena at least twice what is in use, so
+// that the device-side promotions of the call find free slots.
+int grow_pools(gk_set* h, hipStream_t s) {
+  int rc = settle(h, s, false);
+  if (rc) return rc;
+  for (int c = 1; c < h->st.nclass; ++c) {
+    const int64_t used = h->h_ctr ? h->h_ctr[GK_CTR_USED + c] : 0;
+    if (2 * used > h->st.alloc[c]) {
+      int rc = grow_class(h, c, std::max<int64_t>(4 * used, 2 * (int64_t)h->st.alloc[c]), s);
+      if (rc) return rc;
+    }
+  }
+  // presort workspace: what the last completed call needed (its long streams
+  // flushed unsorted if it did not fit -- same results, slower)
+  if (h->ps.ws_need && h->h_ws_need && *h->h_ws_need > h->ps.ws_cap) {
+    const int64_t need = *h->h_ws_need;
+    const int64_t cap = std::max<int64_t>(need + need / 8, 1 << 20);
+    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(hipStreamSynchronize(h->aux));
+    if (h->ps.ws) (void)hipFree(h->ps.ws);
+    h->ps.ws = nullptr;
+    h->ps.ws_cap = 0;
+    if (hipMalloc(&h->ps.ws, (size_t)cap * sizeof(double)) == hipSuccess) {
+      h->ps.ws_cap = cap;
+    } else {
+      h->ps.ws = nullptr;  // not fatal: long streams flush unsorted
+      (void)hipGetLastError();
+    }
+  }
   return GK_OK;
 }
 
-// Read back the overflow list of the last launch(es); returns count (>= 0) or
-// error.  The count and the first kOvfPrefix entries come back in one copy
-// (one synchronisation); a longer list takes a second copy.
-int64_t read_overflow(gk_set* h, std::vector<int32_t>& out, hipStream_t stream) {
-  const int64_t pre = std::min<int64_t>(h->S, kOvfPrefix);
-  if (hipMemcpyAsync(h->h_ovf, h->d_ovf, (1 + pre) * sizeof(int32_t), hipMemcpyDeviceToHost, stream) != hipSuccess ||
+// Return (and clear) an asynchronous error of an earlier call.
+int take_sticky(gk_set* h) {
+  if (h->sticky == GK_OK) return GK_OK;
+  const int rc = h->sticky;
+  g_err = h->sticky_msg;
+  h->sticky = GK_OK;
+  h->sticky_msg.clear();
+  return rc;
+}
+
+// End of a call's device work on `s`: counters -> pinned host memory.
+int mark_done(gk_set* h, hipStream_t s) {
+  HIP_TRY(hipMemcpyAsync(h->h_ctr, h->d_ctr, GK_CTR_WORDS * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipEventRecord(h->ev_done, s));
+  h->done_pending = true;
+  return GK_OK;
+}
+
+int32_t* ovf_count(gk_set* h, int r) { return h->d_ovfc + r; }
+int32_t* ovf_list(gk_set* h, int r) { return h->d_ovfl[r]; }
+
+// Read back round r's overflow count and list (synchronises; merge / import only).
+int64_t read_overflow(gk_set* h, int r, hipStream_t stream) {
+  if (hipMemcpyAsync(h->h_ovf, h->d_ovfc + r, sizeof(int32_t), hipMemcpyDeviceToHost, stream) != hipSuccess ||
       hipStreamSynchronize(stream) != hipSuccess)
     return fail(GK_E_HIP, "overflow readback failed: %s", hipGetErrorString(hipGetLastError()));
-  const int32_t cnt = h->h_ovf[0];
-  out.resize(cnt);
-  if (cnt) {
-    if (cnt <= pre) {
-      std::copy(h->h_ovf + 1, h->h_ovf + 1 + cnt, out.begin());
-    } else if (hipMemcpyAsync(out.data(), h->d_ovf_list, cnt * sizeof(int32_t), hipMemcpyDeviceToHost, stream) !=
-                   hipSuccess ||
-               hipStreamSynchronize(stream) != hipSuccess) {
-      return fail(GK_E_HIP, "overflow list readback failed");
-    }
-    std::sort(out.begin(), out.end());
-  }
-  return cnt;
-}
-
-// Move the listed streams (all currently below class `ncls`) to class `ncls`.
-int promote(gk_set* h, const std::vector<int32_t>& ids, int ncls, hipStream_t stream) {
-  if (ids.empty()) return GK_OK;
-  if (ncls >= h->st.nclass)
-    return fail(GK_E_OVERFLOW, "%zu stream(s) exceed the largest table capacity (%d entries)", ids.size(),
-                h->st.cap[h->st.nclass - 1]);
-  int rc = ensure_slots(h, ncls, h->slots_used[ncls] + (int64_t)ids.size(), stream);
-  if (rc) return rc;
-  rc = ensure_tmp(h, (int64_t)ids.size());
-  if (rc) return rc;
-  if (h->st.cap[ncls] > kMaxLdsCap) {
-    rc = ensure_ws(h);
-    if (rc) return rc;
-  }
-  // host sources of the copies below stay alive until the caller's next
-  // synchronisation (ids: the caller's list; slots: h_slots)
-  std::vector<int32_t>& slots = h->h_slots[ncls];
-  slots.resize(ids.size());
-  for (size_t k = 0; k < ids.size(); ++k) slots[k] = (int32_t)(h->slots_used[ncls] + (int64_t)k);
-  HIP_TRY(hipMemcpyAsync(h->d_tmp_list, ids.data(), ids.size() * sizeof(int32_t), hipMemcpyHostToDevice, stream));
-  HIP_TRY(hipMemcpyAsync(h->d_tmp_slots, slots.data(), slots.size() * sizeof(int32_t), hipMemcpyHostToDevice,
-                         stream));
-  HIP_TRY(gk_launch_promote(h->st, h->d_tmp_list, (int64_t)ids.size(), h->d_tmp_slots, ncls, stream));
-  h->slots_used[ncls] += (int64_t)ids.size();
-  for (int32_t s : ids) {
-    const int old = h->h_cls[s];
-    if (old > 0) {  // leaves its old class list (its old slot is not reused)
-      auto& m = h->members[old];
-      m.erase(std::remove(m.begin(), m.end(), s), m.end());
-    }
-    h->h_cls[s] = (int8_t)ncls;
-    h->members[ncls].push_back(s);
-  }
-  for (int c = 1; c < h->st.nclass; ++c) {
-    rc = sync_list(h, c, stream);
-    if (rc) return rc;
-  }
-  return GK_OK;
+  return h->h_ovf[0];
 }
 
 int check_set(const gk_set* h) {
@@ -238,12 +313,24 @@ int check_set(const gk_set* h) {
   return GK_OK;
 }
 
+hipEvent_t timing_event(std::vector<hipEvent_t>& v, size_t& n) {
+  if (n == v.size()) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    v.push_back(e);
+  }
+  return v[n++];
+}
+
 bool stats_fused(const gk_set* h);
 
-hipError_t launch_class(gk_set* h, int c, const double* x, const int64_t* offs, const int32_t* list, int64_t count,
-                        int force, const GKQuery& q, hipStream_t stream, bool prio = false) {
-  return gk_launch_ingest(h->st.cap[c], h->vpl, h->st, x, offs, list, count, force, h->d_ws, h->ws_bytes,
-                          h->ws_blocks, h->d_ovf_count, h->d_ovf_list, q, h->d_work,
+// One launch of class c: every stream (c == 0) or the streams of `list`
+// whose length is *count_ptr (device).  Overflowing streams go to round r's list.
+hipError_t launch_class(gk_set* h, int c, const double* x, const int64_t* offs, const int32_t* list,
+                        const int32_t* count_ptr, int r, int force, const GKQuery& q, hipStream_t stream,
+                        bool prio = false) {
+  return gk_launch_ingest(h->st.cap[c], h->vpl, h->st, x, offs, list, list ? 0 : h->S, count_ptr, c, force, h->d_ws,
+                          h->ws_bytes, h->ws_blocks, ovf_count(h, r), ovf_list(h, r), q, h->d_work,
                           prio ? h->d_long_list : nullptr, prio ? h->d_long_count : nullptr,
                           prio && h->ps.ws ? h->ps.ws : nullptr, prio && h->ps.ws ? h->ps.list_ws : nullptr,
                           (prio && c == 0 && stats_fused(h)) ? h->fused_stats : 0, stream);
@@ -260,7 +347,8 @@ hipError_t launch_class(gk_set* h, int c, const double* x, const int64_t* offs, 
 bool stats_fused(const gk_set* h) { return h->fused_stats > 0 && h->st.cap[0] == GK_SMALL_CAP; }
 
 int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s) {
-  if (h->timing) HIP_TRY(hipEventRecord(h->ev[2], s));
+  hipEvent_t t0 = h->timing ? timing_event(h->tev_stats, h->n_stats) : nullptr;
+  if (t0) HIP_TRY(hipEventRecord(t0, s));
   // k_stats + k_long_prep, then the fork (k_stats_long needs only the
   // sorted list and the pre-call n), then the presort of the long streams'
   // flush batches on `s`
@@ -272,121 +360,84 @@ int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s) {
   HIP_TRY(hipEventRecord(h->ev_join, h->aux));
   HIP_TRY(gk_launch_presort(h->st, x, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->ps, s));
   if (h->ps.ws_need) HIP_TRY(hipMemcpyAsync(h->h_ws_need, h->ps.ws_need, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  if (h->timing) HIP_TRY(hipEventRecord(h->ev[3], s));
+  hipEvent_t t1 = h->timing ? timing_event(h->tev_stats, h->n_stats) : nullptr;
+  if (t1) HIP_TRY(hipEventRecord(t1, s));
   return GK_OK;
 }
-
-int grow_presort(gk_set* h, hipStream_t s);
 
 int stats_join(gk_set* h, hipStream_t s, const GKQuery& q) {
   HIP_TRY(hipStreamWaitEvent(s, h->ev_join, 0));
-  int rc = grow_presort(h, s);
-  if (rc) return rc;
   HIP_TRY(gk_launch_query_list(h->st, h->d_long_list, h->d_long_count, q, s));
-  if (h->timing) {
-    float ms = 0;
-    HIP_TRY(hipEventElapsedTime(&ms, h->ev[2], h->ev[3]));
-    h->stats_ms += ms;
-  }
   return GK_OK;
 }
 
-// Launch the ingest/flush kernel over every stream (class 0 over all, each
-// larger class over its member list); streams that overflow their class were
-// not committed, so they are promoted one class up and run again.
-// The presort workspace is sized from what the previous call needed (read
-// back after the call; a call whose batches do not fit runs those streams
-// unsorted -- same results, slower flushes).
-int grow_presort(gk_set* h, hipStream_t s) {
-  if (!h->ps.ws_need) return GK_OK;
-  HIP_TRY(hipStreamSynchronize(s));  // the ingest launches synchronise anyway
-  const int64_t need = *h->h_ws_need;
-  if (need <= h->ps.ws_cap) return GK_OK;
-  const int64_t cap = std::max<int64_t>(need + need / 8, 1 << 20);
-  if (h->ps.ws) (void)hipFree(h->ps.ws);
-  h->ps.ws = nullptr;
-  h->ps.ws_cap = 0;
-  if (hipMalloc(&h->ps.ws, (size_t)cap * sizeof(double)) != hipSuccess) {
-    h->ps.ws = nullptr;  // not fatal: long streams flush unsorted
-    (void)hipGetLastError();
-    return GK_OK;
+// The ingest / flush launches of one call, with no host round trip: class 0
+// over every stream and each larger class over its member list; a stream
+// that outgrows its class is not committed, moves one class up on the device
+// (k_promote_dev) and runs again there, at most once per class; a stream
+// with no class left is counted as fatal (reported by a later call).
+// Promotion rounds of a call: round r-1's overflow list moves one class up
+// on the device and runs again in its new class (round r).
+int promote_rounds(gk_set* h, const double* x, const int64_t* offs, int force, const GKQuery& q, hipStream_t stream) {
+  const int R = h->st.nclass;
+  const GKPoolDev pool = pool_args(h);
+  for (int r = 1; r <= R; ++r) {
+    HIP_TRY(hipMemsetAsync(h->d_ctr + GK_CTR_RCNT, 0, GK_MAX_CLASSES * sizeof(int32_t), stream));
+    HIP_TRY(gk_launch_promote_dev(h->st, ovf_count(h, r - 1), ovf_list(h, r - 1), -1, pool, stream));
+    if (r == R) break;  // the last promotion only counts what no class can hold
+    for (int c = r; c < R; ++c)
+      HIP_TRY(launch_class(h, c, x, offs, h->d_rerun[c], h->d_ctr + GK_CTR_RCNT + c, r, force, q, stream));
   }
-  h->ps.ws_cap = cap;
   return GK_OK;
 }
 
 int run_ingest(gk_set* h, const double* x, const int64_t* offs, int force, hipStream_t stream,
                const GKQuery& q = GKQuery(), bool prio = false) {
   if (!offs) offs = h->d_zero_offs;
-  HIP_TRY(hipMemsetAsync(h->d_ovf_count, 0, sizeof(int32_t), stream));
-  // timing covers the class-0 batch launch of gk_ingest (force == 0) only
+  const int R = h->st.nclass;
+  h->last.x = x;
+  h->last.offs = offs;
+  h->last.force = force;
+  h->last.q = q;
+  h->last.may_defer = false;
+  for (int c = 1; c < R; ++c) h->last.may_defer |= h->st.alloc[c] < h->S;
+  HIP_TRY(hipMemsetAsync(h->d_ovfc, 0, kRounds * sizeof(int32_t), stream));
+  HIP_TRY(hipMemsetAsync(h->d_ctr + GK_CTR_DEFER, 0, sizeof(int32_t), stream));
+  // timing covers the class-0 batch launch of gk_ingest (x given) only
   const bool timed = h->timing && x != nullptr;
-  if (timed) HIP_TRY(hipEventRecord(h->ev[0], stream));
-  HIP_TRY(launch_class(h, 0, x, offs, nullptr, h->S, force, q, stream, prio && x != nullptr));
-  if (timed) HIP_TRY(hipEventRecord(h->ev[1], stream));
-  for (int c = 1; c < h->st.nclass; ++c)
-    if (!h->members[c].empty())
-      HIP_TRY(launch_class(h, c, x, offs, h->d_list[c], (int64_t)h->members[c].size(), force, q, stream));
-  std::vector<int32_t> ovf;
-  int64_t cnt = read_overflow(h, ovf, stream);
-  if (cnt < 0) return (int)cnt;
-  if (timed) {
-    float ms = 0;
-    HIP_TRY(hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
-    h->flush_ms += ms;
-    h->launches += 1;
-  }
-  while (!ovf.empty()) {
-    // group by target class
-    std::vector<int32_t> by[GK_MAX_CLASSES];
-    for (int32_t s : ovf) {
-      const int nc = h->h_cls[s] + 1;
-      if (nc >= h->st.nclass)
-        return fail(GK_E_OVERFLOW, "stream %d exceeds the largest table capacity (%d entries)", s,
-                    h->st.cap[h->st.nclass - 1]);
-      by[nc].push_back(s);
-    }
-    HIP_TRY(hipMemsetAsync(h->d_ovf_count, 0, sizeof(int32_t), stream));
-    for (int c = 1; c < h->st.nclass; ++c) {
-      if (by[c].empty()) continue;
-      int rc = promote(h, by[c], c, stream);  // leaves by[c] in d_tmp_list
-      if (rc) return rc;
-      HIP_TRY(launch_class(h, c, x, offs, h->d_tmp_list, (int64_t)by[c].size(), force, q, stream));
-    }
-    cnt = read_overflow(h, ovf, stream);
-    if (cnt < 0) return (int)cnt;
-  }
-  return GK_OK;
+  hipEvent_t t0 = timed ? timing_event(h->tev_flush, h->n_flush) : nullptr;
+  if (t0) HIP_TRY(hipEventRecord(t0, stream));
+  HIP_TRY(launch_class(h, 0, x, offs, nullptr, nullptr, 0, force, q, stream, prio && x != nullptr));
+  hipEvent_t t1 = timed ? timing_event(h->tev_flush, h->n_flush) : nullptr;
+  if (t1) HIP_TRY(hipEventRecord(t1, stream));
+  for (int c = 1; c < R; ++c)
+    HIP_TRY(launch_class(h, c, x, offs, h->d_list[c], h->d_ctr + GK_CTR_LCNT + c, 0, force, q, stream));
+  return promote_rounds(h, x, offs, force, q, stream);
 }
 
 // Merge / explicit merge_compress at LDS capacity level 0, then the streams
-// that did not fit at increasing levels (promoting their dst class as needed).
+// that did not fit at increasing levels (their class raised on the device).
+// Synchronous (one readback per level).
 int run_merge(gk_set* dst, const MergeArgsHost& base, hipStream_t s) {
   MergeArgsHost a = base;
-  a.ovf_count = dst->d_ovf_count;
-  a.ovf_list = dst->d_ovf_list;
-  std::vector<int32_t> todo;
-  // host source of promote()'s async copies: outlives them (the next
-  // read_overflow synchronises the stream), like gk_import's `by`
-  std::vector<int32_t> up;
+  const GKPoolDev pool = pool_args(dst);
+  int64_t todo = 0;
+  HIP_TRY(hipMemsetAsync(dst->d_ovfc, 0, kRounds * sizeof(int32_t), s));
   for (int level = 0; level < dst->st.nclass; ++level) {
     const int cap = dst->st.cap[level];
-    if (level > 0 && todo.empty()) break;
     if (level > 0) {
-      // streams below this class are promoted so that their output may grow
-      up.clear();
-      for (int32_t id : todo)
-        if (dst->h_cls[id] < level) up.push_back(id);
-      int rc = promote(dst, up, level, s);
+      if (todo == 0) return GK_OK;
+      // streams below this class move up so that their output may grow
+      int rc = grow_class(dst, level, (int64_t)dst->st.alloc[level] + todo, s);
       if (rc) return rc;
-      rc = ensure_tmp(dst, (int64_t)todo.size());
-      if (rc) return rc;
-      HIP_TRY(hipMemcpyAsync(dst->d_tmp_list, todo.data(), todo.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
+      HIP_TRY(gk_launch_promote_dev(dst->st, ovf_count(dst, level - 1), ovf_list(dst, level - 1), level, pool, s));
     }
     a.dst = dst->st;
     a.cap = cap;
-    a.list = level == 0 ? nullptr : dst->d_tmp_list;
-    a.count = level == 0 ? dst->S : (int64_t)todo.size();
+    a.list = level == 0 ? nullptr : ovf_list(dst, level - 1);
+    a.count = level == 0 ? dst->S : todo;
+    a.ovf_count = ovf_count(dst, level);
+    a.ovf_list = ovf_list(dst, level);
     if (cap > kMaxLdsCap) {
       int rc = ensure_ws(dst);
       if (rc) return rc;
@@ -398,13 +449,12 @@ int run_merge(gk_set* dst, const MergeArgsHost& base, hipStream_t s) {
       a.ws_bytes = 0;
       a.ws_blocks = 0;
     }
-    HIP_TRY(hipMemsetAsync(dst->d_ovf_count, 0, sizeof(int32_t), s));
     HIP_TRY(gk_launch_merge(a, s));
-    int64_t c = read_overflow(dst, todo, s);
-    if (c < 0) return (int)c;
-    if (c == 0) return GK_OK;
+    todo = read_overflow(dst, level, s);
+    if (todo < 0) return (int)todo;
+    if (todo == 0) return GK_OK;
   }
-  return fail(GK_E_OVERFLOW, "%zu stream(s) exceed %d table entries in merge", todo.size(),
+  return fail(GK_E_OVERFLOW, "%lld stream(s) exceed %d table entries in merge", (long long)todo,
               dst->st.cap[dst->st.nclass - 1]);
 }
 
@@ -479,10 +529,23 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
   st.rtab_n = kRecipTable;
   okm &= hipMalloc(&st.rtab, (size_t)st.rtab_n * sizeof(double)) == hipSuccess;
   okm &= hipMalloc(&st.n0, S * sizeof(int64_t)) == hipSuccess;
-  okm &= hipMalloc(&h->d_ovf, (S + 1) * sizeof(int32_t)) == hipSuccess;
-  okm &= hipHostMalloc(&h->h_ovf, (std::min<int64_t>(S, kOvfPrefix) + 1) * sizeof(int32_t)) == hipSuccess;
-  h->d_ovf_count = h->d_ovf;
-  h->d_ovf_list = h->d_ovf ? h->d_ovf + 1 : nullptr;
+  okm &= hipMalloc(&h->d_ovfc, kRounds * sizeof(int32_t)) == hipSuccess;
+  for (int r = 0; r < kRounds; ++r) okm &= hipMalloc(&h->d_ovfl[r], S * sizeof(int32_t)) == hipSuccess;
+  okm &= hipHostMalloc(&h->h_ovf, 16 * sizeof(int32_t)) == hipSuccess;
+  okm &= hipMalloc(&h->d_ctr, GK_CTR_WORDS * sizeof(int32_t)) == hipSuccess;
+  okm &= hipHostMalloc(&h->h_ctr, GK_CTR_WORDS * sizeof(int32_t)) == hipSuccess;
+  okm &= hipMalloc(&h->d_defer, S * sizeof(int32_t)) == hipSuccess;
+  if (h->h_ctr) memset(h->h_ctr, 0, GK_CTR_WORDS * sizeof(int32_t));
+  okm &= hipEventCreateWithFlags(&h->ev_done, hipEventDisableTiming) == hipSuccess;
+  okm &= hipEventCreateWithFlags(&h->ev_qs, hipEventDisableTiming) == hipSuccess;
+  st.alloc[0] = (int32_t)S;
+  for (int c = 1; c < st.nclass; ++c) {
+    okm &= hipMalloc(&h->d_list[c], S * sizeof(int32_t)) == hipSuccess;
+    okm &= hipMalloc(&h->d_rerun[c], S * sizeof(int32_t)) == hipSuccess;
+    const int64_t n = initial_slots(h, c);
+    okm &= hipMalloc(&st.tab[c], (size_t)n * st.cap[c] * sizeof(GKRec)) == hipSuccess;
+    st.alloc[c] = (int32_t)n;
+  }
   okm &= hipMalloc(&h->d_zero_offs, (S + 1) * sizeof(int64_t)) == hipSuccess;
   okm &= hipMalloc(&h->d_work, GK_WORK_BYTES) == hipSuccess;
   okm &= hipMalloc(&h->d_long_list, S * sizeof(int32_t)) == hipSuccess;
@@ -502,12 +565,12 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
     gk_destroy(h);
     return fail(GK_E_NOMEM, "device allocation for %lld streams failed", (long long)num_streams);
   }
-  h->h_cls.assign((size_t)S, 0);
-  if (st.cap[0] > kMaxLdsCap && ensure_ws(h) != GK_OK) {
+  if (ensure_ws(h) != GK_OK) {  // the global-workspace class may be entered inside any call
     gk_destroy(h);
     return GK_E_NOMEM;
   }
   if (hipMemset(st.cls, 0, S * sizeof(int32_t)) != hipSuccess ||
+      hipMemset(h->d_ctr, 0, GK_CTR_WORDS * sizeof(int32_t)) != hipSuccess ||
       hipMemset(h->d_zero_offs, 0, (S + 1) * sizeof(int64_t)) != hipSuccess ||
       hipMemset(st.slot, 0, S * sizeof(int32_t)) != hipSuccess || gk_launch_reset(st, nullptr) != hipSuccess ||
       gk_launch_rtab(st, nullptr) != hipSuccess ||
@@ -515,30 +578,30 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
     gk_destroy(h);
     return fail(GK_E_HIP, "state initialisation failed");
   }
-  for (auto& e : h->ev) (void)hipEventCreate(&e);
   *out = h;
   return GK_OK;
 }
 
 int gk_destroy(gk_set* h) {
   if (!h) return GK_OK;
-  if (h->aux) (void)hipStreamSynchronize(h->aux);  // k_stats_long may still read the set
+  (void)hipDeviceSynchronize();  // launches of this set may still be running on the caller's stream
   GKState& st = h->st;
-  void* ptrs[] = {st.n,       st.E,           st.pend,          st.mn,          st.mx,         st.sum,
-                  st.avg,     st.cls,         st.slot,          st.tab[0],      st.tab[1],     st.tab[2],
-                  st.pbuf,    h->d_list[0],   h->d_list[1],     h->d_list[2],   h->d_qs,       h->d_ovf,
-                  h->d_tmp_list, h->d_tmp_slots, h->d_ws, h->d_zero_offs, h->d_work,
-                  h->d_long_list, h->d_long_n, h->d_long_count, h->ps.list_ws, h->ps.list_b0, h->ps.ws,
-                  h->ps.ws_need, st.rtab, st.n0};
+  void* ptrs[] = {st.n,       st.E,          st.pend,        st.mn,          st.mx,          st.sum,
+                  st.avg,     st.cls,        st.slot,        st.tab[0],      st.tab[1],      st.tab[2],
+                  st.pbuf,    h->d_list[1],  h->d_list[2],   h->d_rerun[1],  h->d_rerun[2],  h->d_qs,
+                  h->d_ovfc,  h->d_ovfl[0],  h->d_ovfl[1],   h->d_ovfl[2],   h->d_ovfl[3],   h->d_ctr,
+                  h->d_ws,    h->d_zero_offs, h->d_work,     h->d_long_list, h->d_long_n,    h->d_long_count,
+                  h->ps.list_ws, h->ps.list_b0, h->ps.ws,    h->ps.ws_need,  st.rtab,        st.n0,
+                  h->d_defer};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
-  for (auto& e : h->ev)
+  for (auto* v : {&h->tev_flush, &h->tev_stats})
+    for (hipEvent_t e : *v) (void)hipEventDestroy(e);
+  for (hipEvent_t e : {h->ev_fork, h->ev_join, h->ev_done, h->ev_qs})
     if (e) (void)hipEventDestroy(e);
-  if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
-  if (h->ev_join) (void)hipEventDestroy(h->ev_join);
   if (h->aux) (void)hipStreamDestroy(h->aux);
-  if (h->h_ws_need) (void)hipHostFree(h->h_ws_need);
-  if (h->h_ovf) (void)hipHostFree(h->h_ovf);
+  for (void* p : {(void*)h->h_ws_need, (void*)h->h_ovf, (void*)h->h_ctr, (void*)h->h_qs})
+    if (p) (void)hipHostFree(p);
   delete h;
   return GK_OK;
 }
@@ -548,14 +611,14 @@ int gk_reset(gk_set* h, void* stream) {
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   const int64_t S = std::max<int64_t>(h->S, 1);
+  rc = settle(h, s, false);  // a deferred re-run of the last call must not land after the reset
+  if (rc) return rc;
   HIP_TRY(hipMemsetAsync(h->st.cls, 0, S * sizeof(int32_t), s));
   HIP_TRY(hipMemsetAsync(h->st.slot, 0, S * sizeof(int32_t), s));
+  // slots, member lists and re-run lists start over (FATAL stays cumulative:
+  // a readback still in flight carries it)
+  HIP_TRY(hipMemsetAsync(h->d_ctr, 0, GK_CTR_FATAL * sizeof(int32_t), s));
   HIP_TRY(gk_launch_reset(h->st, s));
-  for (int c = 0; c < GK_MAX_CLASSES; ++c) {
-    h->members[c].clear();
-    h->slots_used[c] = 0;
-  }
-  std::fill(h->h_cls.begin(), h->h_cls.end(), 0);
   return GK_OK;
 }
 
@@ -566,18 +629,36 @@ int gk_ingest(gk_set* h, const double* values, const int64_t* offsets, void* str
   if (!values) return fail(GK_E_ARG, "values is null");
   if (h->S == 0) return GK_OK;
   hipStream_t s = (hipStream_t)stream;
+  rc = grow_pools(h, s);
+  if (!rc) rc = take_sticky(h);
+  if (rc) return rc;
   rc = stats_fork(h, values, offsets, s);
   if (rc) return rc;
   rc = run_ingest(h, values, offsets, 0, s, GKQuery(), true);
   const int rj = stats_join(h, s, GKQuery());  // joined on every path
-  return rc ? rc : rj;
+  const int rd = mark_done(h, s);
+  return rc ? rc : (rj ? rj : rd);
 }
 
 int gk_flush(gk_set* h, void* stream) {
   int rc = check_set(h);
   if (rc) return rc;
   if (h->S == 0) return GK_OK;
-  return run_ingest(h, nullptr, nullptr, 1, (hipStream_t)stream);
+  hipStream_t s = (hipStream_t)stream;
+  rc = grow_pools(h, s);
+  if (!rc) rc = take_sticky(h);
+  if (rc) return rc;
+  rc = run_ingest(h, nullptr, nullptr, 1, s);
+  const int rd = mark_done(h, s);
+  return rc ? rc : rd;
+}
+
+int gk_sync(gk_set* h, void* stream) {
+  int rc = check_set(h);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  rc = settle(h, (hipStream_t)stream, true);
+  return rc ? rc : take_sticky(h);
 }
 
 // quantile arguments -> device copy of qs and the effective mode
@@ -595,14 +676,26 @@ static int prepare_query(gk_set* h, const double* qs, int nq, double* out, int m
         break;
       }
   }
+  // the previous call's copy out of h_qs (and its kernels' reads of d_qs,
+  // ordered on the same stream) must not see the new values
+  HIP_TRY(hipEventSynchronize(h->ev_qs));
   if (nq > h->qs_alloc) {
+    HIP_TRY(hipStreamSynchronize(s));
     if (h->d_qs) (void)hipFree(h->d_qs);
+    if (h->h_qs) (void)hipHostFree(h->h_qs);
     h->d_qs = nullptr;
+    h->h_qs = nullptr;
     const int cap = std::max(nq, 64);
-    if (hipMalloc(&h->d_qs, cap * sizeof(double)) != hipSuccess) return fail(GK_E_NOMEM, "qs allocation failed");
+    if (hipMalloc(&h->d_qs, cap * sizeof(double)) != hipSuccess ||
+        hipHostMalloc(&h->h_qs, cap * sizeof(double)) != hipSuccess)
+      return fail(GK_E_NOMEM, "qs allocation failed");
     h->qs_alloc = cap;
   }
-  if (nq) HIP_TRY(hipMemcpyAsync(h->d_qs, qs, nq * sizeof(double), hipMemcpyHostToDevice, s));
+  if (nq) {
+    memcpy(h->h_qs, qs, nq * sizeof(double));
+    HIP_TRY(hipMemcpyAsync(h->d_qs, h->h_qs, nq * sizeof(double), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipEventRecord(h->ev_qs, s));
+  }
   q->qs = nq ? h->d_qs : nullptr;
   q->nq = nq;
   q->out = out;
@@ -618,12 +711,14 @@ int gk_quantiles(gk_set* h, const double* qs, int nq, double* out, int mode, voi
   rc = prepare_query(h, qs, nq, out, mode, s, &q);
   if (rc) return rc;
   if (nq == 0 || h->S == 0) return GK_OK;
+  rc = grow_pools(h, s);
+  if (!rc) rc = take_sticky(h);
+  if (rc) return rc;
   // gk:197-198: pending values are flushed first (state mutation); the
   // quantiles are answered in the same launch from the flushed table
   rc = run_ingest(h, nullptr, nullptr, 1, s, q);
-  if (rc) return rc;
-  HIP_TRY(hipStreamSynchronize(s));
-  return GK_OK;
+  const int rd = mark_done(h, s);
+  return rc ? rc : rd;
 }
 
 int gk_ingest_quantiles(gk_set* h, const double* values, const int64_t* offsets, const double* qs, int nq,
@@ -638,16 +733,17 @@ int gk_ingest_quantiles(gk_set* h, const double* values, const int64_t* offsets,
   if (rc) return rc;
   if (h->S == 0) return GK_OK;
   if (nq == 0) return gk_ingest(h, values, offsets, stream);
+  rc = grow_pools(h, s);
+  if (!rc) rc = take_sticky(h);
+  if (rc) return rc;
   rc = stats_fork(h, values, offsets, s);
   if (rc) return rc;
   // add every value (gk:49-61), then quantiles() (gk:187-232): flush the
   // leftover pending values and answer from the LDS-resident table
   rc = run_ingest(h, values, offsets, 1, s, q, true);
   const int rj = stats_join(h, s, q);  // joined on every path
-  if (rc) return rc;
-  if (rj) return rj;
-  HIP_TRY(hipStreamSynchronize(s));
-  return GK_OK;
+  const int rd = mark_done(h, s);
+  return rc ? rc : (rj ? rj : rd);
 }
 
 int gk_stats(gk_set* h, int64_t* n, double* mn, double* mx, double* sum, double* avg, int32_t* table_size,
@@ -680,10 +776,16 @@ int gk_merge(gk_set* dst, gk_set* const* srcs, int nsrcs, void* stream) {
       return fail(GK_E_ARG, "stream counts differ (%lld vs %lld)", (long long)srcs[k]->S, (long long)dst->S);
   }
   hipStream_t s = (hipStream_t)stream;
+  rc = gk_sync(dst, stream);
+  if (rc) return rc;
   for (int k = 0; k < nsrcs; ++k) {
     gk_set* src = srcs[k];
+    rc = gk_sync(src, stream);
+    if (rc) return rc;
     // other.merge_compress() -- unconditional in the reference (gk:126, 137)
     rc = run_ingest(src, nullptr, nullptr, 2, s);
+    if (!rc) rc = mark_done(src, s);
+    if (!rc) rc = gk_sync(src, stream);
     if (rc) return rc;
     MergeArgsHost a{};
     a.src = src->st;
@@ -701,6 +803,8 @@ int gk_merge_compress(gk_set* h, const double* v, const int32_t* g, const int32_
   if (rc) return rc;
   if (!eoffs || !v || !g || !d) return fail(GK_E_ARG, "null record arrays");
   hipStream_t s = (hipStream_t)stream;
+  rc = gk_sync(h, stream);
+  if (rc) return rc;
   MergeArgsHost a{};
   a.src = h->st;
   a.ev = v;
@@ -757,32 +861,167 @@ int gk_import(gk_set* h, const int64_t* offs, const double* v, const int32_t* g,
   hipStream_t s = (hipStream_t)stream;
   const int64_t S = h->S;
   if (S == 0) return GK_OK;
+  rc = gk_sync(h, stream);
+  if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(h->st.n, n, S * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
   HIP_TRY(hipMemcpyAsync(h->st.mn, mn, S * sizeof(double), hipMemcpyDeviceToDevice, s));
   HIP_TRY(hipMemcpyAsync(h->st.mx, mx, S * sizeof(double), hipMemcpyDeviceToDevice, s));
   HIP_TRY(hipMemcpyAsync(h->st.sum, sum, S * sizeof(double), hipMemcpyDeviceToDevice, s));
   HIP_TRY(hipMemcpyAsync(h->st.avg, avg, S * sizeof(double), hipMemcpyDeviceToDevice, s));
-  std::vector<int32_t> ovf;
-  std::vector<int32_t> by[GK_MAX_CLASSES];  // outlives the copies promote() enqueues from it
+  // tables that do not fit their stream's class: one class up (on the
+  // device) and import again, until every table fits
+  const GKPoolDev pool = pool_args(h);
   for (int round = 0; round <= h->st.nclass; ++round) {
-    HIP_TRY(hipMemsetAsync(h->d_ovf_count, 0, sizeof(int32_t), s));
-    HIP_TRY(gk_launch_import(h->st, offs, v, g, d, poffs, pv, h->d_ovf_count, h->d_ovf_list, s));
-    int64_t c = read_overflow(h, ovf, s);
+    HIP_TRY(hipMemsetAsync(h->d_ovfc, 0, sizeof(int32_t), s));
+    HIP_TRY(gk_launch_import(h->st, offs, v, g, d, poffs, pv, ovf_count(h, 0), ovf_list(h, 0), s));
+    const int64_t c = read_overflow(h, 0, s);
     if (c < 0) return (int)c;
     if (c == 0) return GK_OK;
-    for (auto& b : by) b.clear();
-    for (int32_t id : ovf) {
-      const int nc = h->h_cls[id] + 1;
-      if (nc >= h->st.nclass)
-        return fail(GK_E_OVERFLOW, "imported table of stream %d exceeds %d entries", id, h->st.cap[h->st.nclass - 1]);
-      by[nc].push_back(id);
-    }
-    for (int c2 = 1; c2 < h->st.nclass; ++c2) {
-      rc = promote(h, by[c2], c2, s);
+    for (int k = 1; k < h->st.nclass; ++k) {
+      rc = grow_class(h, k, (int64_t)h->st.alloc[k] + c, s);
       if (rc) return rc;
     }
+    HIP_TRY(gk_launch_promote_dev(h->st, ovf_count(h, 0), ovf_list(h, 0), -2, pool, s));
+    rc = mark_done(h, s);
+    if (!rc) rc = gk_sync(h, stream);
+    if (rc) return rc;
   }
   return fail(GK_E_OVERFLOW, "import did not converge");
+}
+
+// ---- versioned state files (gk_format.h) ------------------------------------
+namespace {
+
+int fmt_error(int rc, const char* path) {
+  switch (rc) {
+    case gkfmt::E_IO: return fail(GK_E_IO, "cannot read/write state file %s", path);
+    case gkfmt::E_VERSION: return fail(GK_E_FORMAT, "%s: unsupported state format version", path);
+    case gkfmt::E_CHECKSUM: return fail(GK_E_FORMAT, "%s: checksum mismatch (corrupt state file)", path);
+    default: return fail(GK_E_FORMAT, "%s: not a GKSTATE file or truncated", path);
+  }
+}
+
+// device scratch freed on scope exit (after the stream was synchronised)
+struct DevBuf {
+  void* p = nullptr;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  bool alloc(size_t bytes) { return hipMalloc(&p, bytes ? bytes : 8) == hipSuccess; }
+};
+
+}  // namespace
+
+int gk_save(gk_set* h, const char* path, void* stream) {
+  int rc = check_set(h);
+  if (rc) return rc;
+  if (!path) return fail(GK_E_ARG, "path is null");
+  rc = gk_sync(h, stream);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t S = h->S;
+  gkfmt::State st;
+  st.eps = h->eps;
+  st.resize_streams(S);
+  if (S) {
+    HIP_TRY(hipMemcpyAsync(st.sizes.data(), h->st.E, S * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(st.psizes.data(), h->st.pend, S * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(st.n.data(), h->st.n, S * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(st.mn.data(), h->st.mn, S * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(st.mx.data(), h->st.mx, S * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(st.sum.data(), h->st.sum, S * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(st.avg.data(), h->st.avg, S * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+  }
+  std::vector<int64_t> offs(S + 1, 0), poffs(S + 1, 0);
+  for (int64_t k = 0; k < S; ++k) {
+    offs[k + 1] = offs[k] + st.sizes[k];
+    poffs[k + 1] = poffs[k] + st.psizes[k];
+  }
+  const int64_t E = offs[S], P = poffs[S];
+  st.v.resize(E);
+  st.g.resize(E);
+  st.d.resize(E);
+  st.pv.resize(P);
+  if (S) {
+    DevBuf d_offs, d_poffs, d_v, d_g, d_d, d_pv;
+    if (!d_offs.alloc((S + 1) * 8) || !d_poffs.alloc((S + 1) * 8) || !d_v.alloc(E * 8) || !d_g.alloc(E * 4) ||
+        !d_d.alloc(E * 4) || !d_pv.alloc(P * 8))
+      return fail(GK_E_NOMEM, "save: device scratch of %lld records failed", (long long)E);
+    HIP_TRY(hipMemcpyAsync(d_offs.p, offs.data(), (S + 1) * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_poffs.p, poffs.data(), (S + 1) * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(gk_launch_export(h->st, (const int64_t*)d_offs.p, (double*)d_v.p, (int32_t*)d_g.p, (int32_t*)d_d.p, s));
+    HIP_TRY(gk_launch_export_pending(h->st, (const int64_t*)d_poffs.p, (double*)d_pv.p, s));
+    if (E) {
+      HIP_TRY(hipMemcpyAsync(st.v.data(), d_v.p, E * 8, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipMemcpyAsync(st.g.data(), d_g.p, E * 4, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipMemcpyAsync(st.d.data(), d_d.p, E * 4, hipMemcpyDeviceToHost, s));
+    }
+    if (P) HIP_TRY(hipMemcpyAsync(st.pv.data(), d_pv.p, P * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+  }
+  rc = gkfmt::write(path, st);
+  return rc ? fmt_error(rc, path) : GK_OK;
+}
+
+int gk_peek(const char* path, double* eps, int64_t* num_streams) {
+  if (!path) return fail(GK_E_ARG, "path is null");
+  gkfmt::Header hd;
+  const int rc = gkfmt::peek(path, &hd);
+  if (rc) return fmt_error(rc, path);
+  if (eps) *eps = hd.eps;
+  if (num_streams) *num_streams = hd.S;
+  return GK_OK;
+}
+
+int gk_load(gk_set* h, const char* path, void* stream) {
+  int rc = check_set(h);
+  if (rc) return rc;
+  if (!path) return fail(GK_E_ARG, "path is null");
+  gkfmt::State st;
+  rc = gkfmt::read(path, &st);
+  if (rc) return fmt_error(rc, path);
+  if (st.S != h->S)
+    return fail(GK_E_ARG, "%s holds %lld streams, the set has %lld", path, (long long)st.S, (long long)h->S);
+  if (st.eps != h->eps) return fail(GK_E_EPS_MISMATCH, "%s was saved with eps=%.17g, the set has eps=%.17g", path,
+                                   st.eps, h->eps);
+  const int64_t S = st.S;
+  if (S == 0) return GK_OK;
+  hipStream_t s = (hipStream_t)stream;
+  std::vector<int64_t> offs(S + 1, 0), poffs(S + 1, 0);
+  for (int64_t k = 0; k < S; ++k) {
+    offs[k + 1] = offs[k] + st.sizes[k];
+    poffs[k + 1] = poffs[k] + st.psizes[k];
+    if (st.psizes[k] >= h->P) return fail(GK_E_FORMAT, "%s: stream %lld holds %d pending values (flush period %d)",
+                                          path, (long long)k, st.psizes[k], h->P);
+  }
+  const int64_t E = offs[S], P = poffs[S];
+  DevBuf d_offs, d_poffs, d_v, d_g, d_d, d_pv, d_hdr;
+  if (!d_offs.alloc((S + 1) * 8) || !d_poffs.alloc((S + 1) * 8) || !d_v.alloc(E * 8) || !d_g.alloc(E * 4) ||
+      !d_d.alloc(E * 4) || !d_pv.alloc(P * 8) || !d_hdr.alloc(5 * S * 8))
+    return fail(GK_E_NOMEM, "load: device scratch of %lld records failed", (long long)E);
+  int64_t* d_n = (int64_t*)d_hdr.p;
+  double* d_f = (double*)d_hdr.p + S;
+  HIP_TRY(hipMemcpyAsync(d_offs.p, offs.data(), (S + 1) * 8, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(d_poffs.p, poffs.data(), (S + 1) * 8, hipMemcpyHostToDevice, s));
+  if (E) {
+    HIP_TRY(hipMemcpyAsync(d_v.p, st.v.data(), E * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_g.p, st.g.data(), E * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_d.p, st.d.data(), E * 4, hipMemcpyHostToDevice, s));
+  }
+  if (P) HIP_TRY(hipMemcpyAsync(d_pv.p, st.pv.data(), P * 8, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(d_n, st.n.data(), S * 8, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(d_f, st.mn.data(), S * 8, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(d_f + S, st.mx.data(), S * 8, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(d_f + 2 * S, st.sum.data(), S * 8, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(d_f + 3 * S, st.avg.data(), S * 8, hipMemcpyHostToDevice, s));
+  rc = gk_import(h, (const int64_t*)d_offs.p, (const double*)d_v.p, (const int32_t*)d_g.p, (const int32_t*)d_d.p,
+                 (const int64_t*)d_poffs.p, (const double*)d_pv.p, d_n, d_f, d_f + S, d_f + 2 * S, d_f + 3 * S,
+                 stream);
+  const hipError_t e = hipStreamSynchronize(s);  // the scratch above is freed on return
+  if (rc) return rc;
+  if (e != hipSuccess) return fail(GK_E_HIP, "load: %s", hipGetErrorString(e));
+  return GK_OK;
 }
 
 int64_t gk_num_streams(const gk_set* h) { return h ? h->S : -1; }
@@ -793,8 +1032,12 @@ int gk_capacity(const gk_set* h, int cls) {
 }
 int64_t gk_num_promoted(const gk_set* h) {
   if (!h) return -1;
+  if (h->S == 0) return 0;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  std::vector<int32_t> cls(h->S);
+  if (hipMemcpy(cls.data(), h->st.cls, h->S * sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess) return -1;
   int64_t n = 0;
-  for (int c = 1; c < GK_MAX_CLASSES; ++c) n += (int64_t)h->members[c].size();
+  for (int32_t c : cls) n += c > 0;
   return n;
 }
 
@@ -808,11 +1051,23 @@ int gk_timing_enable(gk_set* h, int on) {
 int gk_timing_read(gk_set* h, double* flush_ms, double* stats_ms, int64_t* launches) {
   int rc = check_set(h);
   if (rc) return rc;
-  if (flush_ms) *flush_ms = h->flush_ms;
-  if (stats_ms) *stats_ms = h->stats_ms;
-  if (launches) *launches = h->launches;
-  h->flush_ms = h->stats_ms = 0;
-  h->launches = 0;
+  double f = 0, st = 0;
+  for (size_t k = 0; k + 1 < h->n_flush; k += 2) {
+    float ms = 0;
+    HIP_TRY(hipEventSynchronize(h->tev_flush[k + 1]));
+    HIP_TRY(hipEventElapsedTime(&ms, h->tev_flush[k], h->tev_flush[k + 1]));
+    f += ms;
+  }
+  for (size_t k = 0; k + 1 < h->n_stats; k += 2) {
+    float ms = 0;
+    HIP_TRY(hipEventSynchronize(h->tev_stats[k + 1]));
+    HIP_TRY(hipEventElapsedTime(&ms, h->tev_stats[k], h->tev_stats[k + 1]));
+    st += ms;
+  }
+  if (flush_ms) *flush_ms = f;
+  if (stats_ms) *stats_ms = st;
+  if (launches) *launches = (int64_t)(h->n_flush / 2);
+  h->n_flush = h->n_stats = 0;
   return GK_OK;
 }
 

@@ -1207,10 +1207,15 @@ __global__ __launch_bounds__(64) void k_query_list(GKState st, const int32_t* __
 // CAP > 0: LDS working storage of that capacity (class 256 / 2048).
 // CAP == 0: global workspace `ws` (ws_bytes per block) of capacity `cap`.
 // list == NULL: every class-0 stream; else the listed streams (class c > 0).
+// count_ptr (device, may be NULL): the list length is read from there (lists
+// built on the device: promotion re-runs, class member lists).  lcls: the
+// class this launch serves; a listed stream now in another class (promoted
+// further since it was listed) is skipped.
 template <int CAP, int VPL>
 __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restrict__ x,
                                                const int64_t* __restrict__ offs,
                                                const int32_t* __restrict__ list, int64_t count,
+                                               const int32_t* __restrict__ count_ptr, int lcls,
                                                int force, int cap, unsigned char* ws, size_t ws_bytes,
                                                int32_t* __restrict__ ovf_count,
                                                int32_t* __restrict__ ovf_list, const double* __restrict__ qs,
@@ -1246,6 +1251,7 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
   // (k_sort_long) -- so that the long sequential flush chains start at once;
   // items [npri, npri+count) are the launch's streams in order, minus those
   // already taken from `prio` (the same length test k_stats applied).
+  if (count_ptr) count = *count_ptr;
   const int64_t npri = prio ? (int64_t)*prio_count : 0;
   const int64_t total = npri + count;
   auto grab = [&]() -> int64_t {
@@ -1276,7 +1282,7 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
     const double smx = __longlong_as_double(rfl64(__double_as_longlong(hv.mx)));
     if (wn < total) gk_hdr_issue(hv, st, offs, sid(wn));
     w = wn;
-    if (!list && scls != 0) continue;  // promoted: handled by its class launch
+    if (scls != lcls) continue;  // in another class: handled by that class's launch
     const int64_t Lx = xe - xo;
     if (prio && !from_prio && Lx > GK_STATS_LONG) continue;  // taken from `prio`
 
@@ -2834,6 +2840,58 @@ __global__ void k_promote(GKState st, const int32_t* __restrict__ list, int64_t 
   }
 }
 
+// Device-side promotion (no host round trip): every stream on the list
+// (count from the device) moves to class t = cls+1 (level < 0: an ingest
+// overflow) or t = level when it is below that class (level >= 0: a merge at
+// capacity level `level`).  Its slot comes from the class's device counter;
+// the table is copied over, the stream joins the class member list and, for
+// ingest, the re-run list of this round.  The stream's state was not
+// committed, so it stays as it is when it cannot move: no free slot in its
+// next class -> the defer list (the host grows the arena and re-runs it before
+// the set's next call); no class above -> ctr[GK_CTR_FATAL], reported as a
+// (sticky) GK_E_OVERFLOW.
+__global__ void k_promote_dev(GKState st, const int32_t* __restrict__ count, const int32_t* __restrict__ list,
+                              int level, GKPoolDev pool) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int64_t cnt = *count;
+  for (int64_t w = wave; w < cnt; w += nw) {
+    const int64_t s = list[w];
+    const int c = st.cls[s];
+    const int t = level < 0 ? c + 1 : level;  // -1: ingest overflow, -2: import overflow
+    if (level >= 0 && c >= t) continue;      // already large enough
+    int slot = -1;
+    if (lane == 0) {
+      if (t < st.nclass) {
+        slot = atomicAdd(&pool.ctr[GK_CTR_USED + t], 1);
+        if (slot >= st.alloc[t]) {
+          atomicSub(&pool.ctr[GK_CTR_USED + t], 1);
+          slot = -1;
+          if (level == -1) pool.defer[atomicAdd(&pool.ctr[GK_CTR_DEFER], 1)] = (int32_t)s;
+          else atomicAdd(&pool.ctr[GK_CTR_FATAL], 1);  // (merge / import grow the arena first)
+        }
+      } else {
+        atomicAdd(&pool.ctr[GK_CTR_FATAL], 1);
+        atomicMax(&pool.ctr[GK_CTR_FATAL + 1], (int)s);
+      }
+    }
+    slot = __shfl(slot, 0, 64);
+    if (slot < 0) continue;
+    const GKRec* src = gk_table_ptr(st, s);
+    GKRec* dst = st.tab[t] + (int64_t)slot * st.cap[t];
+    const int E = min(st.E[s], st.cap[c]);
+    for (int j = lane; j < E; j += 64) dst[j] = src[j];
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+      st.cls[s] = t;
+      st.slot[s] = slot;
+      pool.list[t][atomicAdd(&pool.ctr[GK_CTR_LCNT + t], 1)] = (int32_t)s;
+      if (level == -1) pool.rerun[t][atomicAdd(&pool.ctr[GK_CTR_RCNT + t], 1)] = (int32_t)s;
+    }
+  }
+}
+
 // ===========================================================================
 // host-side launchers (called from gk_capi.cpp)
 // ===========================================================================
@@ -2854,12 +2912,13 @@ int gk_num_cu() { return num_cu(); }
 
 template <int CAP, int VPL>
 static hipError_t launch_ingest_t(const GKState& st, const double* x, const int64_t* offs,
-                                  const int32_t* list, int64_t count, int force, int cap,
+                                  const int32_t* list, int64_t count, const int32_t* count_ptr, int lcls,
+                                  int force, int cap,
                                   unsigned char* ws, size_t ws_bytes, int64_t ws_blocks,
                                   int32_t* ovf_count, int32_t* ovf_list, const GKQuery& q,
                                   unsigned long long* work, const int32_t* prio, const int32_t* prio_count,
                                   const double* psort, const int64_t* prio_ws, hipStream_t stream) {
-  if (count <= 0) return hipSuccess;
+  if (count <= 0 && !count_ptr) return hipSuccess;
   if (!work) return hipErrorInvalidValue;
   int64_t grid;
   if (CAP > 0) {
@@ -2871,24 +2930,25 @@ static hipError_t launch_ingest_t(const GKState& st, const double* x, const int6
   } else {
     grid = ws_blocks;
   }
-  if (!prio && grid > count) grid = count;
+  if (!prio && !count_ptr && grid > count) grid = count;
   if (grid < 1) grid = 1;
   hipError_t e = hipMemsetAsync(work, 0, sizeof(unsigned long long), stream);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((k_ingest<CAP, VPL>), dim3((unsigned)grid), dim3(64), 0, stream, st, x, offs, list,
-                     count, force, cap, ws, ws_bytes, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode, work,
-                     prio, prio_count, psort, prio_ws);
+                     count, count_ptr, lcls, force, cap, ws, ws_bytes, ovf_count, ovf_list, q.qs, q.nq, q.out,
+                     q.mode, work, prio, prio_count, psort, prio_ws);
   return hipGetLastError();
 }
 
 template <int CAP>
 static hipError_t launch_ingest_vpl(int vpl, const GKState& st, const double* x, const int64_t* offs,
-                                    const int32_t* list, int64_t count, int force, int cap, unsigned char* ws,
+                                    const int32_t* list, int64_t count, const int32_t* count_ptr, int lcls,
+                                    int force, int cap, unsigned char* ws,
                                     size_t ws_bytes, int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list,
                                     const GKQuery& q, unsigned long long* work, const int32_t* prio,
                                     const int32_t* prio_count, const double* psort, const int64_t* prio_ws,
                                     hipStream_t stream) {
-#define GK_L(V) launch_ingest_t<CAP, V>(st, x, offs, list, count, force, cap, ws, ws_bytes, ws_blocks, \
+#define GK_L(V) launch_ingest_t<CAP, V>(st, x, offs, list, count, count_ptr, lcls, force, cap, ws, ws_bytes, ws_blocks, \
                                         ovf_count, ovf_list, q, work, prio, prio_count, psort, prio_ws, stream)
   switch (vpl) {
     case 1: return GK_L(1);
@@ -2936,24 +2996,26 @@ static hipError_t launch_ingest_small(const GKState& st, const double* x, const 
 size_t gk_ingest_ws_bytes(int cap, int vpl) { return gk_flush_ws_bytes(cap, vpl); }
 
 hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x, const int64_t* offs,
-                            const int32_t* list, int64_t count, int force, unsigned char* ws, size_t ws_bytes,
+                            const int32_t* list, int64_t count, const int32_t* count_ptr, int lcls, int force,
+                            unsigned char* ws, size_t ws_bytes,
                             int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list, const GKQuery& q,
                             unsigned long long* work, const int32_t* prio, const int32_t* prio_count,
                             const double* psort, const int64_t* prio_ws, int fused_stats, hipStream_t stream) {
   switch (cap) {
     case SMALL_CAP:
+      if (list || count_ptr || lcls != 0) return hipErrorInvalidValue;  // class 0 over every stream only
       if (vpl == 1)
         return launch_ingest_small<1>(st, x, offs, list, count, force, ovf_count, ovf_list, q, work, fused_stats, stream);
       if (vpl == 2)
         return launch_ingest_small<2>(st, x, offs, list, count, force, ovf_count, ovf_list, q, work, fused_stats, stream);
       return hipErrorInvalidValue;
     case 2048:
-      return launch_ingest_vpl<2048>(vpl, st, x, offs, list, count, force, cap, nullptr, 0, 0, ovf_count, ovf_list,
-                                     q, work, prio, prio_count, psort, prio_ws, stream);
+      return launch_ingest_vpl<2048>(vpl, st, x, offs, list, count, count_ptr, lcls, force, cap, nullptr, 0, 0,
+                                     ovf_count, ovf_list, q, work, prio, prio_count, psort, prio_ws, stream);
     default:
       if (!ws || ws_blocks <= 0) return hipErrorInvalidValue;
-      return launch_ingest_vpl<0>(vpl, st, x, offs, list, count, force, cap, ws, ws_bytes, ws_blocks, ovf_count,
-                                  ovf_list, q, work, prio, prio_count, psort, prio_ws, stream);
+      return launch_ingest_vpl<0>(vpl, st, x, offs, list, count, count_ptr, lcls, force, cap, ws, ws_bytes,
+                                  ws_blocks, ovf_count, ovf_list, q, work, prio, prio_count, psort, prio_ws, stream);
   }
 }
 
@@ -3083,6 +3145,13 @@ hipError_t gk_launch_import(const GKState& st, const int64_t* offs, const double
   if (st.S <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_import, dim3((unsigned)wave_grid(st.S)), dim3(256), 0, stream, st, offs, v, g, d,
                      poffs, pv, ovf_count, ovf_list);
+  return hipGetLastError();
+}
+
+hipError_t gk_launch_promote_dev(const GKState& st, const int32_t* count, const int32_t* list, int level,
+                                 const GKPoolDev& pool, hipStream_t stream) {
+  hipLaunchKernelGGL(k_promote_dev, dim3((unsigned)(num_cu() * 2)), dim3(256), 0, stream, st, count, list, level,
+                     pool);
   return hipGetLastError();
 }
 

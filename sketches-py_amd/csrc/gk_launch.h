@@ -43,8 +43,11 @@ size_t gk_ingest_ws_bytes(int cap, int vpl);
 #define GK_WORK_BYTES 1152  // 8 hand-out counters + the stats-role batch counter, one 128-byte line each
 // `work`: GK_WORK_BYTES of device counters of the small-class launch (dynamic stream hand-out).
 // cap GK_SMALL_CAP / 2048: LDS kernels; any other cap: global workspace ws (ws_bytes per block, ws_blocks blocks)
+// list/count (host count) or list/count_ptr (device count): the streams of a class-lcls launch
+// (list NULL: every stream, class 0); listed streams no longer in class lcls are skipped.
 hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x, const int64_t* offs,
-                            const int32_t* list, int64_t count, int force, unsigned char* ws, size_t ws_bytes,
+                            const int32_t* list, int64_t count, const int32_t* count_ptr, int lcls, int force,
+                            unsigned char* ws, size_t ws_bytes,
                             int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list, const GKQuery& q,
                             unsigned long long* work, const int32_t* prio, const int32_t* prio_count,
                             const double* psort, const int64_t* prio_ws, int fused_stats, hipStream_t stream);
@@ -94,3 +97,24 @@ hipError_t gk_launch_import(const GKState& st, const int64_t* offs, const double
                             int32_t* ovf_list, hipStream_t stream);
 hipError_t gk_launch_promote(const GKState& st, const int32_t* list, int64_t count, const int32_t* slots, int ncls,
                              hipStream_t stream);
+
+// Device-side capacity-class bookkeeping: counters (slots used, member list
+// lengths, re-run list lengths, streams that found no class / slot) and, per
+// class c > 0, its member list and this round's re-run list (S entries each).
+#define GK_CTR_USED 0
+#define GK_CTR_LCNT 4
+#define GK_CTR_RCNT 8
+#define GK_CTR_FATAL 12   // [12] count, [13] largest such stream id
+#define GK_CTR_DEFER 14   // streams whose class had no free slot this call (re-run by the host later)
+#define GK_CTR_WORDS 16
+struct GKPoolDev {
+  int32_t* ctr;
+  int32_t* list[GK_MAX_CLASSES];
+  int32_t* rerun[GK_MAX_CLASSES];
+  int32_t* defer;  // S entries
+};
+// k_promote_dev over list[0 .. *count): level -1 -> class cls+1 (ingest
+// overflow: joins the re-run list, or the defer list when that class has no
+// free slot), -2 -> class cls+1 (import), level >= 0 -> class `level` if below it
+hipError_t gk_launch_promote_dev(const GKState& st, const int32_t* count, const int32_t* list, int level,
+                                 const GKPoolDev& pool, hipStream_t stream);

@@ -37,6 +37,7 @@ struct GKState {
   int32_t* slot;    // slot of stream s inside its class arena
   GKRec* tab[GK_MAX_CLASSES];
   int32_t cap[GK_MAX_CLASSES];
+  int32_t alloc[GK_MAX_CLASSES];  // slots allocated in tab[c] (c > 0; class 0: S)
   int32_t nclass;
 
   double* pbuf;     // pending values: pbuf + s*pmax, insertion order

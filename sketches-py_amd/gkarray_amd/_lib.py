@@ -10,7 +10,7 @@ import os
 
 __all__ = ["lib", "load", "GKBackendError", "check", "LIB_PATH", "SYMBOLS",
            "GK_OK", "GK_E_ARG", "GK_E_EPS_MISMATCH", "GK_E_OVERFLOW", "GK_E_HIP",
-           "GK_E_NOMEM", "GK_E_UNSUPPORTED", "GK_Q_LIST", "GK_Q_SINGLE"]
+           "GK_E_NOMEM", "GK_E_UNSUPPORTED", "GK_E_IO", "GK_E_FORMAT", "GK_Q_LIST", "GK_Q_SINGLE"]
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgkarray_hip.so")
 
@@ -21,6 +21,8 @@ GK_E_OVERFLOW = -3
 GK_E_HIP = -4
 GK_E_NOMEM = -5
 GK_E_UNSUPPORTED = -6
+GK_E_IO = -7
+GK_E_FORMAT = -8
 GK_Q_LIST = 0
 GK_Q_SINGLE = 1
 
@@ -48,6 +50,7 @@ SYMBOLS = {
     "gk_reset": (_INT, [_P, _P]),
     "gk_ingest": (_INT, [_P, _P, _P, _P]),
     "gk_flush": (_INT, [_P, _P]),
+    "gk_sync": (_INT, [_P, _P]),
     "gk_quantiles": (_INT, [_P, ctypes.POINTER(_D), _INT, _P, _INT, _P]),
     "gk_ingest_quantiles": (_INT, [_P, _P, _P, ctypes.POINTER(_D), _INT, _P, _INT, _P]),
     "gk_stats": (_INT, [_P, _P, _P, _P, _P, _P, _P, _P, _P]),
@@ -58,6 +61,9 @@ SYMBOLS = {
     "gk_export_pending_sizes": (_INT, [_P, _P, _P]),
     "gk_export_pending": (_INT, [_P, _P, _P, _P]),
     "gk_import": (_INT, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "gk_save": (_INT, [_P, ctypes.c_char_p, _P]),
+    "gk_peek": (_INT, [ctypes.c_char_p, ctypes.POINTER(_D), ctypes.POINTER(_I64)]),
+    "gk_load": (_INT, [_P, ctypes.c_char_p, _P]),
     "gk_num_streams": (_I64, [_P]),
     "gk_eps": (_D, [_P]),
     "gk_flush_period": (_INT, [_P]),

@@ -6,12 +6,22 @@ kernels of ``libgkarray_hip.so`` through the C ABI of ``include/gk_capi.h``;
 PyTorch only allocates device tensors and supplies the current HIP stream.
 """
 import ctypes
+import os
 
 import torch
 
 from . import _lib as L
 
-__all__ = ["StreamSet"]
+__all__ = ["StreamSet", "peek"]
+
+
+def peek(path):
+    """(eps, num_streams) from a GKSTATE file's header."""
+    lib = L.load()
+    eps = ctypes.c_double()
+    S = ctypes.c_int64()
+    L.check(lib.gk_peek(os.fsencode(path), ctypes.byref(eps), ctypes.byref(S)))
+    return eps.value, S.value
 
 
 def _stream_ptr(device):
@@ -91,7 +101,14 @@ class StreamSet:
         with torch.cuda.device(self.device):
             L.check(self._lib.gk_reset(self._h, self._sp()))
 
-    def ingest(self, values, offsets, quantiles=None, single=False):
+    def sync(self):
+        """Wait for this set's work on the current stream; raise an
+        asynchronous error of an earlier call (a stream that outgrew every
+        table capacity class keeps its previous state: GK_E_OVERFLOW)."""
+        with torch.cuda.device(self.device):
+            L.check(self._lib.gk_sync(self._h, self._sp()))
+
+    def ingest(self, values, offsets, quantiles=None, single=False, sync=True):
         """Batched ``GKArray.add`` (gk:49-61) over all streams.
 
         values: float64 [N] (device tensor preferred); offsets: int64 [S+1].
@@ -99,6 +116,9 @@ class StreamSet:
         (gk:187-232) for every stream in the same kernel pass (the leftover
         pending values are flushed, as the reference's quantiles() does) and
         returns the [S, len(qs)] float64 device tensor.
+        ``sync=False`` only enqueues the work on the current HIP stream (the
+        C ABI itself never blocks here); errors then surface at a later call
+        or ``sync()``.
         """
         v = self._dev(values, torch.float64)
         o = self._dev(offsets, torch.int64)
@@ -109,6 +129,8 @@ class StreamSet:
         if quantiles is None:
             with torch.cuda.device(self.device):
                 L.check(self._lib.gk_ingest(self._h, _ptr(v), _ptr(o), self._sp()))
+            if sync:
+                self.sync()
             return None
         qs = [float(q) for q in quantiles]
         nq = len(qs)
@@ -118,6 +140,8 @@ class StreamSet:
         with torch.cuda.device(self.device):
             L.check(self._lib.gk_ingest_quantiles(self._h, _ptr(v), _ptr(o), arr, nq, _ptr(out), mode,
                                                   self._sp()))
+        if sync:
+            self.sync()
         return out[:, :nq]
 
     def ingest_lists(self, seqs):
@@ -135,6 +159,7 @@ class StreamSet:
         """``merge_compress()`` where values are pending (gk:45-46, 166, 197)."""
         with torch.cuda.device(self.device):
             L.check(self._lib.gk_flush(self._h, self._sp()))
+        self.sync()
 
     # ------------------------------------------------------------------ query
     def quantiles(self, qs, single=False):
@@ -152,6 +177,7 @@ class StreamSet:
         mode = L.GK_Q_SINGLE if single else L.GK_Q_LIST
         with torch.cuda.device(self.device):
             L.check(self._lib.gk_quantiles(self._h, arr, nq, _ptr(out), mode, self._sp()))
+        self.sync()
         return out
 
     def stats(self):
@@ -242,6 +268,31 @@ class StreamSet:
                                         _ptr(t["d"]), _ptr(t["poffs"]), _ptr(t["pv"]),
                                         _ptr(t["n"]), _ptr(t["min"]), _ptr(t["max"]),
                                         _ptr(t["sum"]), _ptr(t["avg"]), self._sp()))
+
+    # ------------------------------------------------------------------ files
+    def save(self, path):
+        """Write every stream's state (tables, pending values, n/min/max/sum/avg)
+        to a versioned GKSTATE file (csrc/gk_format.h) without flushing."""
+        with torch.cuda.device(self.device):
+            L.check(self._lib.gk_save(self._h, os.fsencode(path), self._sp()))
+
+    def load_state(self, path):
+        """Replace every stream's state with a GKSTATE file's (same stream
+        count and eps as this set)."""
+        with torch.cuda.device(self.device):
+            rc = self._lib.gk_load(self._h, os.fsencode(path), self._sp())
+        if rc == L.GK_E_EPS_MISMATCH:
+            from .gkarray import UnequalEpsilonException
+            raise UnequalEpsilonException(L.last_error())
+        L.check(rc)
+
+    @classmethod
+    def load(cls, path, device=None):
+        """A new StreamSet holding the state saved in ``path``."""
+        eps, S = peek(path)
+        ss = cls(S, eps, device=device)
+        ss.load_state(path)
+        return ss
 
     # ------------------------------------------------------------------ merge
     def merge_from(self, others):

@@ -1,0 +1,142 @@
+"""Versioned state files on the GPU path (gk_save / gk_load through the C ABI):
+checkpoint mid-stream, restore into a fresh set and continue -- bit-exact vs
+an uninterrupted oracle run; import an oracle-produced state file and continue
+on the GPU; GPU files read by the numpy reader; eps / stream-count mismatch."""
+import numpy as np
+import pytest
+import torch
+
+from gk_oracle_c import OracleSet
+from gkarray_amd import stateio
+from parity_util import _ss, assert_same_quantiles, assert_same_state, csr, gen, small_of
+
+pytestmark = pytest.mark.gpu
+
+
+def batches(S, eps, rng, parts=3):
+    P = int(1.0 / eps) + 1
+    out = []
+    for part in range(parts):
+        lens = rng.integers(0, 6 * P, S)
+        lens[:4] = [0, 1, P - 1, P]
+        seqs = [gen(int(d), int(L), rng) for d, L in zip(rng.integers(0, 8, S), lens)]
+        out.append(csr(seqs))
+    return out
+
+
+@pytest.mark.parametrize("eps", [0.05, 0.01, 0.001])
+def test_checkpoint_restore_continue(gpu_device, tmp_path, eps):
+    from gkarray_amd import StreamSet
+    rng = np.random.default_rng(71 + int(1 / eps))
+    S = 400 if eps >= 0.01 else 80
+    bs = batches(S, eps, rng)
+    o = OracleSet(S, eps)  # uninterrupted
+    a = _ss(S, eps, gpu_device)
+    flat, offs = bs[0]
+    a.ingest(torch.from_numpy(flat), torch.from_numpy(offs))
+    o.ingest(flat, offs)
+    p = str(tmp_path / "ckpt.gks")
+    a.save(p)
+    a.close()
+    b = StreamSet.load(p, device=gpu_device)  # fresh set from the file
+    assert b.num_streams == S and b.eps == eps
+    assert_same_state(b, o, "restored")
+    for flat, offs in bs[1:]:
+        b.ingest(torch.from_numpy(flat), torch.from_numpy(offs))
+        o.ingest(flat, offs)
+        assert_same_state(b, o, "continued")
+    q = b.quantiles([0.1, 0.5, 0.99]).cpu().numpy()
+    assert_same_quantiles(q, o.quantiles([0.1, 0.5, 0.99]), "restored q", small_of(o, eps))
+
+
+def test_import_oracle_state_file(gpu_device, tmp_path):
+    from gkarray_amd import StreamSet
+    eps, S = 0.01, 500
+    rng = np.random.default_rng(73)
+    bs = batches(S, eps, rng, parts=2)
+    o = OracleSet(S, eps)
+    flat, offs = bs[0]
+    o.ingest(flat, offs)
+    to, tv, tg, td = o.tables()
+    po, pv = o.pending()
+    st = o.stats()
+    p = str(tmp_path / "oracle.gks")
+    stateio.write_state(p, dict(eps=eps, offs=to, v=tv, g=tg, d=td, poffs=po, pv=pv, n=st["n"], min=st["min"],
+                                max=st["max"], sum=st["sum"], avg=st["avg"]))
+    g = StreamSet.load(p, device=gpu_device)
+    assert_same_state(g, o, "imported")
+    flat, offs = bs[1]
+    q = g.ingest(torch.from_numpy(flat), torch.from_numpy(offs), quantiles=[0.5, 0.9, 0.99]).cpu().numpy()
+    o.ingest(flat, offs)
+    assert_same_quantiles(q, o.quantiles([0.5, 0.9, 0.99]), "imported q", small_of(o, eps))
+    assert_same_state(g, o, "imported + continued")
+    # and back: the GPU's file, read by the numpy reader, is the oracle's state
+    p2 = str(tmp_path / "gpu.gks")
+    g.save(p2)
+    r = stateio.read_state(p2)
+    to, tv, tg, td = o.tables()
+    assert np.array_equal(r["offs"], to) and np.array_equal(r["v"].view(np.int64), tv.view(np.int64))
+    assert np.array_equal(r["g"], tg) and np.array_equal(r["d"], td)
+    assert np.array_equal(r["avg"].view(np.int64), o.stats()["avg"].view(np.int64))
+
+
+def test_promoted_streams_roundtrip(gpu_device, tmp_path):
+    """Tables beyond the small class (descending streams) survive the file."""
+    from gkarray_amd import StreamSet
+    rng = np.random.default_rng(79)
+    S = 24
+    seqs = [np.sort(rng.random(int(L)))[::-1].copy() for L in rng.integers(20000, 40000, S)]
+    flat, offs = csr(seqs)
+    a = _ss(S, 0.01, gpu_device)
+    a.ingest(torch.from_numpy(flat), torch.from_numpy(offs))
+    o = OracleSet(S, 0.01)
+    o.ingest(flat, offs)
+    assert a.num_promoted > 0
+    p = str(tmp_path / "big.gks")
+    a.save(p)
+    b = StreamSet.load(p, device=gpu_device)
+    assert_same_state(b, o, "promoted restored")
+
+
+def test_load_mismatch_errors(gpu_device, tmp_path):
+    from gkarray_amd import GKBackendError, StreamSet, UnequalEpsilonException
+    a = _ss(10, 0.01, gpu_device)
+    a.ingest(torch.rand(1000, dtype=torch.float64), torch.arange(0, 1001, 100))
+    p = str(tmp_path / "m.gks")
+    a.save(p)
+    with pytest.raises(UnequalEpsilonException):
+        _ss(10, 0.02, gpu_device).load_state(p)
+    with pytest.raises(GKBackendError):
+        _ss(11, 0.01, gpu_device).load_state(p)
+    raw = bytearray(open(p, "rb").read())
+    raw[-3] ^= 0x40
+    open(p, "wb").write(bytes(raw))
+    with pytest.raises(GKBackendError, match="checksum"):
+        StreamSet.load(p, device=gpu_device)
+
+
+@pytest.mark.parametrize("asynchronous", [False, True])
+def test_promotion_arena_exhaustion_defers_and_reruns(gpu_device, monkeypatch, asynchronous):
+    """Capacity-class arenas with 2 slots (GK_POOL_SLOTS): most overflowing
+    streams find no slot in their next class during the call, are deferred on
+    the device and re-run from the call's own inputs before the set's next
+    call (or in sync()).  State must equal the oracle's either way."""
+    monkeypatch.setenv("GK_POOL_SLOTS", "2")
+    rng = np.random.default_rng(83)
+    S = 48
+    ss = _ss(S, 0.01, gpu_device)
+    o = OracleSet(S, 0.01)
+    keep = []
+    for part in range(3):
+        seqs = [np.sort(rng.random(int(L)))[::-1].copy() if k % 3 else rng.random(int(L))
+                for k, L in enumerate(rng.integers(5000, 30000, S))]
+        flat, offs = csr(seqs)
+        tf, to = torch.from_numpy(flat).to(gpu_device), torch.from_numpy(offs).to(gpu_device)
+        keep.append((tf, to))  # inputs stay valid until the next call (async contract)
+        ss.ingest(tf, to, sync=not asynchronous)
+        o.ingest(flat, offs)
+    ss.sync()
+    assert ss.num_promoted > 2
+    assert_same_state(ss, o, "deferred re-run")
+    q = ss.quantiles([0.01, 0.5, 0.99]).cpu().numpy()
+    assert_same_quantiles(q, o.quantiles([0.01, 0.5, 0.99]), "deferred q", small_of(o, 0.01))
