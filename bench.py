@@ -49,9 +49,10 @@ def parse():
     ap.add_argument("--eps", type=float, default=None, help="default 0.01 (cfg5: 0.001)")
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--cpu-sample", type=int, default=1_000_000,
-                    help="streams of the same workload timed on the host oracle (rank 0, N=1); "
+                    help="streams of the same workload timed on the host engine (rank 0, N=1); "
                          "default: the whole cfg3 batch")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, os.cpu_count())")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = the CPUs this process may use (capped by OMP_NUM_THREADS if set)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--exchange", default="allgather", choices=["allgather", "alltoall"],
                     help="cfg4 row-shard exchange over RCCL before the merge fold")
@@ -112,23 +113,58 @@ def algorithmic_bytes(ss, S, N, nq):
             + 8 * nq * S)
 
 
-def cpu_baseline(x, offs, sample, threads, eps, gpu_q):
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    from gk_oracle_c import OracleSet
+def host_cores():
+    """CPUs this process may run on (cgroup / affinity), the machine's count,
+    and the threads the baseline uses: every CPU of the affinity set, capped
+    by OMP_NUM_THREADS when the box sets it (the GPU box's per-GPU CPU share)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    cap = os.environ.get("OMP_NUM_THREADS")
+    threads = min(aff, int(cap)) if cap and cap.isdigit() and int(cap) > 0 else aff
+    return threads, aff, os.cpu_count() or aff
+
+
+def cpu_baseline(x, offs, sample, threads, eps, gpu_q, py_streams=2000):
+    """The reference path on the host, timed on this box (rank 0, N=1):
+    * the product's host engine (libgkarray_cpu.so, StreamSet(device="cpu"),
+      threads over streams) on the first `sample` streams of the same batch --
+      also a parity check of the GPU quantiles on that sample;
+    * the reference algorithm in pure Python on ONE core (oracle/gk_oracle.py,
+      test infrastructure, like-for-like with gkarray.py's own speed: SURVEY 6
+      measured 529k values/s/core) on the first `py_streams` streams."""
+    from gkarray_amd import StreamSet
     o_all = offs[: sample + 1].cpu().numpy()
     nv = int(o_all[-1] - o_all[0])
-    xs = x[int(o_all[0]): int(o_all[-1])].cpu().numpy()
-    o_loc = o_all - o_all[0]
-    o = OracleSet(sample, eps, threads=threads)
+    xs = x[int(o_all[0]): int(o_all[-1])].cpu()
+    o_loc = torch.from_numpy(o_all - o_all[0])
+    hs = StreamSet(sample, eps, device="cpu")
+    hs.set_threads(threads)
     t0 = time.perf_counter()
-    o.ingest(xs, o_loc)
-    q = o.quantiles([0.5, 0.9, 0.99])
+    q = hs.ingest(xs, o_loc, quantiles=[0.5, 0.9, 0.99]).numpy()
     dt = time.perf_counter() - t0
     same = np.array_equal(q.view(np.int64), gpu_q[:sample].view(np.int64))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from gk_oracle import OracleGK
+    ps = min(py_streams, sample)
+    xn = xs.numpy()
+    t1 = time.perf_counter()
+    for s in range(ps):
+        g = OracleGK(eps)
+        g.add_many(xn[o_all[s] - o_all[0]: o_all[s + 1] - o_all[0]].tolist())
+        g.quantiles([0.5, 0.9, 0.99])
+    dpy = time.perf_counter() - t1
+    npy = int(o_all[ps] - o_all[0])
+    _, aff, ncpu = host_cores()
     return dict(value=nv / dt, unit="values/s", cores=threads, kind="port",
-                sample="%d streams, %d values (the first streams of the GPU workload), "
-                       "ingest + quantiles([.5,.9,.99]) in oracle/gk_oracle.c, %.1f s" % (sample, nv, dt),
-                parity_on_sample=bool(same))
+                sample="%d streams, %d values (the first streams of the GPU workload), ingest + "
+                       "quantiles([.5,.9,.99]) in the host engine libgkarray_cpu.so on %d threads, %.2f s"
+                       % (sample, nv, threads, dt),
+                parity_on_sample=bool(same), host_cpus=ncpu, affinity_cpus=aff,
+                python_1core=dict(value=npy / dpy, unit="values/s", cores=1,
+                                  sample="%d streams, %d values, pure-Python restatement of gkarray.py "
+                                         "(oracle/gk_oracle.py), %.2f s" % (ps, npy, dpy)))
 
 
 def main():
@@ -263,7 +299,7 @@ def main():
                      "stats_kernel_ms": stats_ms / max(launches, 1)},
     }
     if rank == 0 and world == 1 and not a.no_cpu and a.workload != "cfg4":
-        threads = a.cpu_threads or min(16, os.cpu_count() or 1)
+        threads = a.cpu_threads or host_cores()[0]
         sample = min(a.cpu_sample, S)
         if a.workload == "cfg5":  # the long streams dominate: a bounded prefix of streams
             sample = min(sample, 20000)

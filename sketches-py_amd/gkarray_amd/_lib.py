@@ -8,11 +8,14 @@ raises ``GKBackendError``.
 import ctypes
 import os
 
-__all__ = ["lib", "load", "GKBackendError", "check", "LIB_PATH", "SYMBOLS",
+__all__ = ["lib", "load", "load_cpu", "GKBackendError", "check", "LIB_PATH", "CPU_LIB_PATH", "SYMBOLS",
+           "CPU_SYMBOLS",
            "GK_OK", "GK_E_ARG", "GK_E_EPS_MISMATCH", "GK_E_OVERFLOW", "GK_E_HIP",
            "GK_E_NOMEM", "GK_E_UNSUPPORTED", "GK_E_IO", "GK_E_FORMAT", "GK_Q_LIST", "GK_Q_SINGLE"]
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgkarray_hip.so")
+# host engine (include/gk_cpu.h): same C ABI on host memory, selected explicitly
+CPU_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgkarray_cpu.so")
 
 GK_OK = 0
 GK_E_ARG = -1
@@ -73,7 +76,34 @@ SYMBOLS = {
     "gk_timing_read": (_INT, [_P, ctypes.POINTER(_D), ctypes.POINTER(_D), ctypes.POINTER(_I64)]),
 }
 
+# the host engine exports every SYMBOLS entry plus these (include/gk_cpu.h)
+CPU_SYMBOLS = dict(SYMBOLS)
+CPU_SYMBOLS.update({
+    "gk_cpu_set_threads": (_INT, [_P, _INT]),
+    "gk_cpu_threads": (_INT, [_P]),
+})
+
 _lib = None
+_cpu_lib = None
+
+
+def load_cpu(path=None):
+    """Load the host engine libgkarray_cpu.so (cached).  Only used when a
+    caller asks for device="cpu"; never a fallback for the HIP library."""
+    global _cpu_lib
+    if _cpu_lib is not None and path is None:
+        return _cpu_lib
+    p = path or CPU_LIB_PATH
+    if not os.path.exists(p):
+        raise GKBackendError(GK_E_ARG, "CPU engine not built: %s (run __graft_entry__.build())" % p)
+    handle = ctypes.CDLL(p)
+    for name, (res, args) in CPU_SYMBOLS.items():
+        fn = getattr(handle, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _cpu_lib = handle
+    return handle
 
 
 def load(path=None):
@@ -102,11 +132,11 @@ def lib():
     return load()
 
 
-def last_error():
-    return load().gk_last_error().decode("utf-8", "replace")
+def last_error(handle=None):
+    return (handle or load()).gk_last_error().decode("utf-8", "replace")
 
 
-def check(rc):
+def check(rc, handle=None):
     if rc != GK_OK:
-        raise GKBackendError(rc, last_error())
+        raise GKBackendError(rc, last_error(handle))
     return rc

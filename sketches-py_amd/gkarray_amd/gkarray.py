@@ -146,6 +146,8 @@ class GKArray:
     def add_many(self, values):
         """Extension: ``for v in values: add(v)`` in one call."""
         self._ship()
+        if not isinstance(values, torch.Tensor):
+            values = np.ascontiguousarray(values, dtype=np.float64)  # any stride / sequence
         t = torch.as_tensor(values, dtype=torch.float64).reshape(-1)
         if t.numel():
             self._set.ingest(t.to(self._set.device),

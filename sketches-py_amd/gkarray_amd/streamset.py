@@ -5,6 +5,7 @@ Every stream behaves exactly like one reference ``GKArray`` (gkarray.py,
 kernels of ``libgkarray_hip.so`` through the C ABI of ``include/gk_capi.h``;
 PyTorch only allocates device tensors and supplies the current HIP stream.
 """
+import contextlib
 import ctypes
 import os
 
@@ -15,16 +16,18 @@ from . import _lib as L
 __all__ = ["StreamSet", "peek"]
 
 
-def peek(path):
+def peek(path, cpu=False):
     """(eps, num_streams) from a GKSTATE file's header."""
-    lib = L.load()
+    lib = L.load_cpu() if cpu else L.load()
     eps = ctypes.c_double()
     S = ctypes.c_int64()
-    L.check(lib.gk_peek(os.fsencode(path), ctypes.byref(eps), ctypes.byref(S)))
+    L.check(lib.gk_peek(os.fsencode(path), ctypes.byref(eps), ctypes.byref(S)), lib)
     return eps.value, S.value
 
 
 def _stream_ptr(device):
+    if device.type != "cuda":
+        return None
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
@@ -40,24 +43,49 @@ class StreamSet:
     """
 
     def __init__(self, num_streams, eps, device=None, cap_hint=0):
-        if not torch.cuda.is_available():
-            raise L.GKBackendError(L.GK_E_HIP, "no GPU visible: the GKArray engine has no CPU path")
-        self._lib = L.load()
-        if device is None:
-            device = torch.device("cuda", torch.cuda.current_device())
-        device = torch.device(device)
-        if device.type != "cuda":
-            raise ValueError("StreamSet needs a cuda (HIP) device, got %s" % device)
-        if device.index is None:
-            device = torch.device("cuda", torch.cuda.current_device())
+        """``device``: a cuda (HIP) device -- the MI355X engine, the default --
+        or ``"cpu"`` for the host engine (libgkarray_cpu.so, same C ABI and
+        results, multi-threaded over streams).  There is no implicit fallback
+        from the GPU to the host engine."""
+        if device is not None and torch.device(device).type == "cpu":
+            self._lib = L.load_cpu()
+            device = torch.device("cpu")
+            dev_index = -1
+        else:
+            if not torch.cuda.is_available():
+                raise L.GKBackendError(L.GK_E_HIP, "no GPU visible (the host engine is StreamSet(..., device='cpu'))")
+            self._lib = L.load()
+            if device is None:
+                device = torch.device("cuda", torch.cuda.current_device())
+            device = torch.device(device)
+            if device.type != "cuda":
+                raise ValueError("StreamSet needs a cuda (HIP) device or 'cpu', got %s" % device)
+            if device.index is None:
+                device = torch.device("cuda", torch.cuda.current_device())
+            dev_index = device.index
         self.device = device
         self.num_streams = int(num_streams)
         self.eps = eps
         h = ctypes.c_void_p()
-        with torch.cuda.device(device):
-            L.check(self._lib.gk_create(self.num_streams, float(eps), int(cap_hint),
-                                        device.index, ctypes.byref(h)))
+        with self._ctx():
+            self._check(self._lib.gk_create(self.num_streams, float(eps), int(cap_hint), dev_index, ctypes.byref(h)))
         self._h = h
+
+    @property
+    def is_cpu(self):
+        return self.device.type == "cpu"
+
+    def _ctx(self):
+        return contextlib.nullcontext() if self.device.type == "cpu" else torch.cuda.device(self.device)
+
+    def _check(self, rc):
+        return L.check(rc, self._lib)
+
+    def set_threads(self, threads):
+        """Host threads of the CPU engine (0 = every CPU this process may use)."""
+        if not self.is_cpu:
+            raise ValueError("set_threads applies to the CPU engine only")
+        self._check(self._lib.gk_cpu_set_threads(self._h, int(threads)))
 
     # ------------------------------------------------------------------ basics
     def close(self):
@@ -98,15 +126,15 @@ class StreamSet:
     # ------------------------------------------------------------------ ingest
     def reset(self):
         """Every stream back to ``GKArray(eps)`` (gk:21-29)."""
-        with torch.cuda.device(self.device):
-            L.check(self._lib.gk_reset(self._h, self._sp()))
+        with self._ctx():
+            self._check(self._lib.gk_reset(self._h, self._sp()))
 
     def sync(self):
         """Wait for this set's work on the current stream; raise an
         asynchronous error of an earlier call (a stream that outgrew every
         table capacity class keeps its previous state: GK_E_OVERFLOW)."""
-        with torch.cuda.device(self.device):
-            L.check(self._lib.gk_sync(self._h, self._sp()))
+        with self._ctx():
+            self._check(self._lib.gk_sync(self._h, self._sp()))
 
     def ingest(self, values, offsets, quantiles=None, single=False, sync=True):
         """Batched ``GKArray.add`` (gk:49-61) over all streams.
@@ -127,8 +155,8 @@ class StreamSet:
         if v.numel() == 0:
             v = torch.zeros(1, dtype=torch.float64, device=self.device)
         if quantiles is None:
-            with torch.cuda.device(self.device):
-                L.check(self._lib.gk_ingest(self._h, _ptr(v), _ptr(o), self._sp()))
+            with self._ctx():
+                self._check(self._lib.gk_ingest(self._h, _ptr(v), _ptr(o), self._sp()))
             if sync:
                 self.sync()
             return None
@@ -137,8 +165,8 @@ class StreamSet:
         out = torch.empty((self.num_streams, max(nq, 1)), dtype=torch.float64, device=self.device)
         arr = (ctypes.c_double * max(nq, 1))(*qs)
         mode = L.GK_Q_SINGLE if single else L.GK_Q_LIST
-        with torch.cuda.device(self.device):
-            L.check(self._lib.gk_ingest_quantiles(self._h, _ptr(v), _ptr(o), arr, nq, _ptr(out), mode,
+        with self._ctx():
+            self._check(self._lib.gk_ingest_quantiles(self._h, _ptr(v), _ptr(o), arr, nq, _ptr(out), mode,
                                                   self._sp()))
         if sync:
             self.sync()
@@ -157,8 +185,8 @@ class StreamSet:
 
     def flush(self):
         """``merge_compress()`` where values are pending (gk:45-46, 166, 197)."""
-        with torch.cuda.device(self.device):
-            L.check(self._lib.gk_flush(self._h, self._sp()))
+        with self._ctx():
+            self._check(self._lib.gk_flush(self._h, self._sp()))
         self.sync()
 
     # ------------------------------------------------------------------ query
@@ -175,8 +203,8 @@ class StreamSet:
             return out[:, :0]
         arr = (ctypes.c_double * nq)(*qs)
         mode = L.GK_Q_SINGLE if single else L.GK_Q_LIST
-        with torch.cuda.device(self.device):
-            L.check(self._lib.gk_quantiles(self._h, arr, nq, _ptr(out), mode, self._sp()))
+        with self._ctx():
+            self._check(self._lib.gk_quantiles(self._h, arr, nq, _ptr(out), mode, self._sp()))
         self.sync()
         return out
 
@@ -193,8 +221,8 @@ class StreamSet:
             size=torch.empty(S, dtype=torch.int32, device=self.device),
             pending=torch.empty(S, dtype=torch.int32, device=self.device),
         )
-        with torch.cuda.device(self.device):
-            L.check(self._lib.gk_stats(self._h, _ptr(d["n"]), _ptr(d["min"]), _ptr(d["max"]),
+        with self._ctx():
+            self._check(self._lib.gk_stats(self._h, _ptr(d["n"]), _ptr(d["min"]), _ptr(d["max"]),
                                        _ptr(d["sum"]), _ptr(d["avg"]), _ptr(d["size"]),
                                        _ptr(d["pending"]), self._sp()))
         if self.num_streams == 0:
@@ -206,8 +234,8 @@ class StreamSet:
         """All tables in CSR form: (offs int64[S+1], v f64, g i32, d i32)."""
         S = self.num_streams
         sizes = torch.empty(max(S, 1), dtype=torch.int32, device=self.device)
-        with torch.cuda.device(self.device):
-            L.check(self._lib.gk_export_sizes(self._h, _ptr(sizes), self._sp()))
+        with self._ctx():
+            self._check(self._lib.gk_export_sizes(self._h, _ptr(sizes), self._sp()))
         sizes = sizes[:S]
         offs = torch.zeros(S + 1, dtype=torch.int64, device=self.device)
         if S:
@@ -216,24 +244,24 @@ class StreamSet:
         v = torch.empty(max(tot, 1), dtype=torch.float64, device=self.device)
         g = torch.empty(max(tot, 1), dtype=torch.int32, device=self.device)
         d = torch.empty(max(tot, 1), dtype=torch.int32, device=self.device)
-        with torch.cuda.device(self.device):
-            L.check(self._lib.gk_export(self._h, _ptr(offs), _ptr(v), _ptr(g), _ptr(d), self._sp()))
+        with self._ctx():
+            self._check(self._lib.gk_export(self._h, _ptr(offs), _ptr(v), _ptr(g), _ptr(d), self._sp()))
         return offs, v[:tot], g[:tot], d[:tot]
 
     def pending(self):
         """All pending (incoming) values in CSR form: (poffs int64[S+1], pv f64)."""
         S = self.num_streams
         sizes = torch.empty(max(S, 1), dtype=torch.int32, device=self.device)
-        with torch.cuda.device(self.device):
-            L.check(self._lib.gk_export_pending_sizes(self._h, _ptr(sizes), self._sp()))
+        with self._ctx():
+            self._check(self._lib.gk_export_pending_sizes(self._h, _ptr(sizes), self._sp()))
         sizes = sizes[:S]
         offs = torch.zeros(S + 1, dtype=torch.int64, device=self.device)
         if S:
             offs[1:] = torch.cumsum(sizes.to(torch.int64), 0)
         tot = int(offs[-1].item()) if S else 0
         pv = torch.empty(max(tot, 1), dtype=torch.float64, device=self.device)
-        with torch.cuda.device(self.device):
-            L.check(self._lib.gk_export_pending(self._h, _ptr(offs), _ptr(pv), self._sp()))
+        with self._ctx():
+            self._check(self._lib.gk_export_pending(self._h, _ptr(offs), _ptr(pv), self._sp()))
         return offs, pv[:tot]
 
     def table(self, s):
@@ -263,8 +291,8 @@ class StreamSet:
         for k in ("v", "g", "d", "pv"):
             if t[k].numel() == 0:
                 t[k] = torch.zeros(1, dtype=t[k].dtype, device=self.device)
-        with torch.cuda.device(self.device):
-            L.check(self._lib.gk_import(self._h, _ptr(t["offs"]), _ptr(t["v"]), _ptr(t["g"]),
+        with self._ctx():
+            self._check(self._lib.gk_import(self._h, _ptr(t["offs"]), _ptr(t["v"]), _ptr(t["g"]),
                                         _ptr(t["d"]), _ptr(t["poffs"]), _ptr(t["pv"]),
                                         _ptr(t["n"]), _ptr(t["min"]), _ptr(t["max"]),
                                         _ptr(t["sum"]), _ptr(t["avg"]), self._sp()))
@@ -273,23 +301,23 @@ class StreamSet:
     def save(self, path):
         """Write every stream's state (tables, pending values, n/min/max/sum/avg)
         to a versioned GKSTATE file (csrc/gk_format.h) without flushing."""
-        with torch.cuda.device(self.device):
-            L.check(self._lib.gk_save(self._h, os.fsencode(path), self._sp()))
+        with self._ctx():
+            self._check(self._lib.gk_save(self._h, os.fsencode(path), self._sp()))
 
     def load_state(self, path):
         """Replace every stream's state with a GKSTATE file's (same stream
         count and eps as this set)."""
-        with torch.cuda.device(self.device):
+        with self._ctx():
             rc = self._lib.gk_load(self._h, os.fsencode(path), self._sp())
         if rc == L.GK_E_EPS_MISMATCH:
             from .gkarray import UnequalEpsilonException
-            raise UnequalEpsilonException(L.last_error())
-        L.check(rc)
+            raise UnequalEpsilonException(L.last_error(self._lib))
+        self._check(rc)
 
     @classmethod
     def load(cls, path, device=None):
         """A new StreamSet holding the state saved in ``path``."""
-        eps, S = peek(path)
+        eps, S = peek(path, cpu=device is not None and torch.device(device).type == "cpu")
         ss = cls(S, eps, device=device)
         ss.load_state(path)
         return ss
@@ -304,13 +332,16 @@ class StreamSet:
             if o.eps != self.eps:
                 from .gkarray import UnequalEpsilonException
                 raise UnequalEpsilonException("Cannot merge two GKArrays with different epsilon values")
+        for o in others:
+            if o.is_cpu != self.is_cpu:
+                raise ValueError("cannot merge a CPU-engine set with a GPU-engine set (export / import the state)")
         arr = (ctypes.c_void_p * max(len(others), 1))(*[o._h for o in others])
-        with torch.cuda.device(self.device):
+        with self._ctx():
             rc = self._lib.gk_merge(self._h, arr, len(others), self._sp())
         if rc == L.GK_E_EPS_MISMATCH:
             from .gkarray import UnequalEpsilonException
             raise UnequalEpsilonException("Cannot merge two GKArrays with different epsilon values")
-        L.check(rc)
+        self._check(rc)
 
     def merge_compress(self, v=None, g=None, d=None, eoffs=None):
         """``merge_compress(entries)`` (gk:63-109) on every stream; stream s
@@ -330,17 +361,17 @@ class StreamSet:
             t_v = torch.zeros(1, dtype=torch.float64, device=self.device)
             t_g = torch.zeros(1, dtype=torch.int32, device=self.device)
             t_d = torch.zeros(1, dtype=torch.int32, device=self.device)
-        with torch.cuda.device(self.device):
-            L.check(self._lib.gk_merge_compress(self._h, _ptr(t_v), _ptr(t_g), _ptr(t_d),
+        with self._ctx():
+            self._check(self._lib.gk_merge_compress(self._h, _ptr(t_v), _ptr(t_g), _ptr(t_d),
                                                 _ptr(t_o), self._sp()))
 
     # ------------------------------------------------------------------ timing
     def timing(self, on=True):
-        L.check(self._lib.gk_timing_enable(self._h, 1 if on else 0))
+        self._check(self._lib.gk_timing_enable(self._h, 1 if on else 0))
 
     def read_timing(self):
         f = ctypes.c_double()
         s = ctypes.c_double()
         n = ctypes.c_int64()
-        L.check(self._lib.gk_timing_read(self._h, ctypes.byref(f), ctypes.byref(s), ctypes.byref(n)))
+        self._check(self._lib.gk_timing_read(self._h, ctypes.byref(f), ctypes.byref(s), ctypes.byref(n)))
         return f.value, s.value, n.value
