@@ -1,12 +1,11 @@
-# A/B of library variants on the default bench workload:  bash scripts/gpu_ab.sh TAG lib1 lib2 ...
-# (libs are file names under sketches-py_amd/gkarray_amd/, built with `make variant`)
+# A/B of library builds on the default bench (cfg3) and cfg2.
+# Usage: gpu_ab.sh TAG "ENV1=.. ENV2=.." "libname1 libname2 ..."   (lib names in sketches-py_amd/gkarray_amd)
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-TAG=${1:-ab}; shift
-WL=${WL:-cfg3}
-for rep in 1 2; do
-for lib in "$@"; do
-  GK_LIB_PATH=$GRAFT_REPO_ROOT/sketches-py_amd/gkarray_amd/$lib timeout -k 10 300 python bench.py --workload $WL --steps 5 --warmup 2 --no-cpu > gpurun_out/${TAG}_$lib.log 2>&1 || exit $?
-  tail -1 gpurun_out/${TAG}_$lib.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('$lib', 'Gv/s=%.2f'%(d['value']/1e9), 'ms/step=%.2f'%d['ms_per_step'], 'ingest_ms=%.2f'%r['launch_ms'], 'stats_ms=%.2f'%r['stats_kernel_ms'], 'GB/s=%.0f'%r['achieved'])"
-done
+TAG=$1; shift
+for cfg in "$@"; do
+  for rep in 1 2; do
+    env $cfg timeout -k 10 300 python bench.py --no-cpu --steps 10 --warmup 3 > gpurun_out/${TAG}_ab.tmp 2>&1 || { echo "FAILED: $cfg"; tail -20 gpurun_out/${TAG}_ab.tmp; exit 1; }
+    python3 -c "import json,sys; d=json.loads(open('gpurun_out/${TAG}_ab.tmp').read().strip().splitlines()[-1]); print('%-60s %7.2f Gv/s  ms/step %.3f  launch_ms %.3f  frac %.3f' % (sys.argv[1], d['value']/1e9, d['ms_per_step'], d['roofline']['launch_ms'], d['roofline']['frac']))" "$cfg" | tee -a gpurun_out/${TAG}_ab.txt
+  done
 done
