@@ -197,14 +197,13 @@ def main():
         if K == 1:
             x, offs = make_input(S, L, a.seed + rank, dev, dist_name)
             ss = StreamSet(S, a.eps, device=dev)
+            # fold sets allocated once; one host size sync per step (dist.RowShardMerger)
+            merger = gd.RowShardMerger(S, a.eps, dev, exchange=a.exchange)
 
             def step():
                 ss.reset()
-                ss.ingest(x, offs)
-                merged, _ = gd.merge_row_shards(ss, exchange=a.exchange)
-                q = merged.quantiles(qs)
-                merged.close()
-                return q
+                ss.ingest(x, offs, sync=False)
+                return merger(ss).quantiles(qs)
         else:
             shards = [make_input(S, L, a.seed + k, dev, dist_name) for k in range(K)]
             sets = [StreamSet(S, a.eps, device=dev) for _ in range(K)]
@@ -213,7 +212,7 @@ def main():
             def step():
                 for (xk, ok), sk in zip(shards, sets):
                     sk.reset()
-                    sk.ingest(xk, ok)
+                    sk.ingest(xk, ok, sync=False)
                 sets[0].merge_from(sets[1:])  # sk0.merge(sk1)...merge(skK-1), gk:111-154
                 return sets[0].quantiles(qs)
     else:

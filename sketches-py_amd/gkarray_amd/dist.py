@@ -25,7 +25,7 @@ import torch.distributed as dist
 
 __all__ = ["stream_range", "balanced_assignment", "pack_state", "unpack_state", "all_gather_varlen",
            "allgather_states", "alltoall_states", "slice_state", "concat_states", "fold_states",
-           "merge_row_shards"]
+           "merge_row_shards", "RowShardMerger"]
 
 _F64 = ("v", "pv", "min", "max", "sum", "avg")
 _I64 = ("offs", "poffs", "n")
@@ -181,6 +181,8 @@ def merge_row_shards(ss, group=None, exchange="allgather"):
     the rows).  Returns (StreamSet over streams [a, b), (a, b)); the fold is in
     rank order, identical to the reference's sk0.merge(sk1)...merge(skN-1).
     `exchange`: "allgather" (north star) or "alltoall" (each table crosses once).
+    One-off form (state dicts, fresh fold sets); repeated exchanges should
+    keep a ``RowShardMerger``, which allocates once and syncs the host once.
     """
     if exchange not in ("alltoall", "allgather"):
         raise ValueError("exchange must be 'alltoall' or 'allgather'")
@@ -197,3 +199,155 @@ def merge_row_shards(ss, group=None, exchange="allgather"):
         else:
             mine = [slice_state(st, a, b) for st in allgather_states(ss.export_state(), group)]
     return fold_states(mine, device=ss.device), (a, b)
+
+
+class RowShardMerger:
+    """Row-shard exchange + rank-ordered fold, built once and reused every step.
+
+    ``merger(ss)``: ``ss`` is this rank's StreamSet over all S streams (its
+    slice of the rows); returns the StreamSet of this rank's stream range
+    [a, b) holding ``sk_0.merge(sk_1)...merge(sk_{N-1})`` (gk:111-154) of every
+    stream in it.  Per call:
+
+    * ONE host synchronisation: each rank's record totals (table entries,
+      pending values) are all-gathered on the device and read back together;
+    * tables are exported on the device straight into buffers padded to the
+      largest rank's totals (the caching allocator reuses them), packed into
+      three flat payloads (f64 / i64 / i32) and all-gathered over RCCL with no
+      further size exchange ("allgather", the north star's exchange); with
+      ``exchange="alltoall"`` every rank receives only its own stream range of
+      each peer (one extra all-gather of range-boundary offsets, same sync);
+    * the N fold sets were allocated at construction: each is filled by
+      ``gk_import`` with offsets that point into the received payload as it is
+      (no slicing on the host), then folded by ``gk_merge`` in rank order.
+    """
+
+    def __init__(self, num_streams, eps, device, group=None, exchange="allgather"):
+        from .streamset import StreamSet
+        if exchange not in ("alltoall", "allgather"):
+            raise ValueError("exchange must be 'alltoall' or 'allgather'")
+        self.S = int(num_streams)
+        self.eps = eps
+        self.device = torch.device(device)
+        self.group = group
+        self.exchange = exchange
+        on = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if on else 1
+        self.rank = dist.get_rank(group) if on else 0
+        self.range = stream_range(self.S, self.world, self.rank)
+        self.bounds = torch.tensor([stream_range(self.S, self.world, r)[0] for r in range(self.world)] + [self.S],
+                                   dtype=torch.int64, device=self.device)
+        n = self.range[1] - self.range[0]
+        self.sets = [StreamSet(n, eps, device=self.device) for _ in range(self.world)]
+
+    def _gather(self, t):
+        if self.world == 1:
+            return [t]
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(out, t, group=self.group)
+        return out
+
+    def __call__(self, ss):
+        S, world, dev = self.S, self.world, self.device
+        a, b = self.range
+        e, p = ss.export_sizes()
+        offs = torch.zeros(S + 1, dtype=torch.int64, device=dev)
+        poffs = torch.zeros(S + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(e.to(torch.int64), 0, out=offs[1:])
+        torch.cumsum(p.to(torch.int64), 0, out=poffs[1:])
+        # record offsets at every rank's range boundary (alltoall splits) -- the
+        # totals are the last ones; one all-gather, one readback
+        eb, pb = offs[self.bounds], poffs[self.bounds]
+        meta = torch.stack(self._gather(torch.cat([eb, pb])))  # [world, 2 (world+1)]
+        meta_h = meta.cpu()  # the one host synchronisation of the exchange
+        W1 = world + 1
+        if self.exchange == "allgather":
+            Emax = int(meta_h[:, W1 - 1].max())
+            Pmax = int(meta_h[:, 2 * W1 - 1].max())
+        else:
+            Emax = Pmax = 0
+        E_loc, P_loc = int(meta_h[self.rank, W1 - 1]), int(meta_h[self.rank, 2 * W1 - 1])
+        v = torch.empty(max(E_loc, Emax, 1), dtype=torch.float64, device=dev)
+        gd = torch.empty(2 * max(E_loc, Emax, 1), dtype=torch.int32, device=dev)
+        pv = torch.empty(max(P_loc, Pmax, 1), dtype=torch.float64, device=dev)
+        nE = v.numel()
+        ss.export_into(offs, v, gd[:nE], gd[nE:], poffs, pv)
+        st = ss.stats()
+        hdr_f = torch.cat([st["min"], st["max"], st["sum"], st["avg"]])
+        hdr_i = torch.cat([offs, poffs, st["n"]])
+        if self.exchange == "allgather":
+            fs = self._gather(torch.cat([v, pv, hdr_f]))
+            is_ = self._gather(hdr_i)
+            js = self._gather(gd)
+            nP = pv.numel()
+            views = []
+            for k in range(world):
+                f, i, j = fs[k], is_[k], js[k]
+                views.append(dict(v=f[:nE], pv=f[nE:nE + nP], hf=f[nE + nP:].view(4, S),
+                                  offs=i[:S + 1], poffs=i[S + 1:2 * S + 2], n=i[2 * S + 2:],
+                                  g=j[:nE], d=j[nE:], lo=a, hi=b))
+        else:
+            views = self._alltoall(meta_h, v[:E_loc], gd[:nE][:E_loc], gd[nE:][:E_loc], pv[:P_loc], hdr_f,
+                                   offs, poffs, st["n"])
+        for k, w in enumerate(views):
+            lo, hi = w["lo"], w["hi"]
+            self.sets[k].import_arrays(w["offs"][lo:hi + 1], w["v"], w["g"], w["d"], w["poffs"][lo:hi + 1],
+                                       w["pv"], w["n"][lo:hi], w["hf"][0, lo:hi], w["hf"][1, lo:hi],
+                                       w["hf"][2, lo:hi], w["hf"][3, lo:hi])
+        if world > 1:
+            self.sets[0].merge_from(self.sets[1:])
+        return self.sets[0]
+
+    def _alltoall(self, meta_h, v, g, d, pv, hdr_f, offs, poffs, n):
+        """Each peer receives exactly its stream range of this rank's state."""
+        S, world, dev, W1 = self.S, self.world, self.device, self.world + 1
+        bnd = [int(x) for x in self.bounds.tolist()]  # static (construction-time) boundaries
+
+        def splits(row, base):  # per destination: records of its range in source `row`
+            return [int(meta_h[row, base + r + 1] - meta_h[row, base + r]) for r in range(world)]
+        e_in, p_in = splits(self.rank, 0), splits(self.rank, W1)
+        e_out = [splits(k, 0)[self.rank] for k in range(world)]
+        p_out = [splits(k, W1)[self.rank] for k in range(world)]
+        hf = hdr_f.view(4, S)
+        n_rng = [bnd[r + 1] - bnd[r] for r in range(world)]
+        a, b = self.range
+        # per destination r: its range's offsets rebased to the records sent to it
+        offs_parts = [offs[bnd[r]:bnd[r + 1] + 1] - offs[bnd[r]] for r in range(world)]
+        poffs_parts = [poffs[bnd[r]:bnd[r + 1] + 1] - poffs[bnd[r]] for r in range(world)]
+        i_send = torch.cat([torch.cat([o, po, n[bnd[r]:bnd[r + 1]]]) for r, (o, po) in
+                            enumerate(zip(offs_parts, poffs_parts))])
+        # f payload per destination: its tables' values, its pending values, its 4 header rows
+        v_parts = list(torch.split(v, e_in))
+        pv_parts = list(torch.split(pv, p_in))
+        f_send = torch.cat([torch.cat([v_parts[r], pv_parts[r], hf[:, bnd[r]:bnd[r + 1]].reshape(-1)])
+                            for r in range(world)])
+        f_in_sizes = [e_in[r] + p_in[r] + 4 * n_rng[r] for r in range(world)]
+        f_out_sizes = [e_out[k] + p_out[k] + 4 * (b - a) for k in range(world)]
+        j_send = torch.cat([torch.cat([gp, dp]) for gp, dp in zip(torch.split(g, e_in), torch.split(d, e_in))])
+        j_in_sizes = [2 * e_in[r] for r in range(world)]
+        j_out_sizes = [2 * e_out[k] for k in range(world)]
+        i_in_sizes = [2 * (n_rng[r] + 1) + n_rng[r] for r in range(world)]
+        i_out_sizes = [2 * (b - a + 1) + (b - a) for _ in range(world)]
+        f_recv = torch.empty(sum(f_out_sizes), dtype=torch.float64, device=dev)
+        i_recv = torch.empty(sum(i_out_sizes), dtype=torch.int64, device=dev)
+        j_recv = torch.empty(max(sum(j_out_sizes), 1), dtype=torch.int32, device=dev)
+        dist.all_to_all_single(f_recv, f_send, output_split_sizes=f_out_sizes, input_split_sizes=f_in_sizes,
+                               group=self.group)
+        dist.all_to_all_single(i_recv, i_send, output_split_sizes=i_out_sizes, input_split_sizes=i_in_sizes,
+                               group=self.group)
+        dist.all_to_all_single(j_recv[:sum(j_out_sizes)], j_send, output_split_sizes=j_out_sizes,
+                               input_split_sizes=j_in_sizes, group=self.group)
+        views = []
+        fo = io = jo = 0
+        m = b - a
+        for k in range(world):
+            f = f_recv[fo:fo + f_out_sizes[k]]
+            i = i_recv[io:io + i_out_sizes[k]]
+            j = j_recv[jo:jo + j_out_sizes[k]]
+            fo, io, jo = fo + f_out_sizes[k], io + i_out_sizes[k], jo + j_out_sizes[k]
+            ek, pk = e_out[k], p_out[k]
+            views.append(dict(v=f[:ek] if ek else f[:1], pv=f[ek:ek + pk] if pk else f[:1],
+                              hf=f[ek + pk:].view(4, m), offs=i[:m + 1], poffs=i[m + 1:2 * m + 2],
+                              n=i[2 * m + 2:], g=j[:ek] if ek else torch.zeros(1, dtype=torch.int32, device=dev),
+                              d=j[ek:2 * ek] if ek else torch.zeros(1, dtype=torch.int32, device=dev), lo=0, hi=m))
+        return views

@@ -322,6 +322,31 @@ class StreamSet:
         ss.load_state(path)
         return ss
 
+    def import_arrays(self, offs, v, g, d, poffs, pv, n, mn, mx, sm, av):
+        """``gk_import`` on device tensors as they are (no copies): stream s's
+        table is ``v/g/d[offs[s]:offs[s+1]]`` -- offsets may be absolute into
+        a larger array (a slice of another set's export) -- and its pending
+        values ``pv[poffs[s]:poffs[s+1]]``; header arrays have S entries."""
+        with self._ctx():
+            self._check(self._lib.gk_import(self._h, _ptr(offs), _ptr(v), _ptr(g), _ptr(d), _ptr(poffs), _ptr(pv),
+                                            _ptr(n), _ptr(mn), _ptr(mx), _ptr(sm), _ptr(av), self._sp()))
+
+    def export_sizes(self):
+        """Device tensors (table sizes int32[S], pending counts int32[S]) -- no host sync."""
+        S = max(self.num_streams, 1)
+        e = torch.empty(S, dtype=torch.int32, device=self.device)
+        p = torch.empty(S, dtype=torch.int32, device=self.device)
+        with self._ctx():
+            self._check(self._lib.gk_export_sizes(self._h, _ptr(e), self._sp()))
+            self._check(self._lib.gk_export_pending_sizes(self._h, _ptr(p), self._sp()))
+        return e[:self.num_streams], p[:self.num_streams]
+
+    def export_into(self, offs, v, g, d, poffs, pv):
+        """Tables / pending values into caller buffers at the given offsets (device, no host sync)."""
+        with self._ctx():
+            self._check(self._lib.gk_export(self._h, _ptr(offs), _ptr(v), _ptr(g), _ptr(d), self._sp()))
+            self._check(self._lib.gk_export_pending(self._h, _ptr(poffs), _ptr(pv), self._sp()))
+
     # ------------------------------------------------------------------ merge
     def merge_from(self, others):
         """Left fold ``self.merge(others[0]); self.merge(others[1]); ...``

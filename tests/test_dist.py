@@ -180,3 +180,60 @@ def test_gpu_fold_of_virtual_row_shards(gpu_device):
     q = acc.quantiles([0.5, 0.9, 0.99]).cpu().numpy()
     rq = ref.quantiles([0.5, 0.9, 0.99])
     assert np.array_equal(q.view(np.int64), rq.view(np.int64))
+
+
+def _merger_worker(rank, world, port, S, eps, exchange, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gkarray_amd import StreamSet
+        flat, offs = shard_data(rank, S, eps)
+        ss = StreamSet(S, eps, device="cpu")  # the host engine: same C ABI as the GPU path
+        merger = gd.RowShardMerger(S, eps, "cpu", exchange=exchange)
+        res = None
+        for step in range(2):  # reused: same fold sets, fresh exchange each step
+            ss.reset()
+            ss.ingest(torch.from_numpy(flat), torch.from_numpy(offs))
+            m = merger(ss)
+            to, v, g, d = (t.clone() for t in m.tables())
+            st = {k: t.clone() for k, t in m.stats().items()}
+            res = (to.tolist(), v.tolist(), g.tolist(), d.tolist(), st["n"].tolist(), st["min"].tolist(),
+                   st["max"].tolist())
+        q.put((rank, merger.range, res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,exchange", [(2, "allgather"), (3, "allgather"), (2, "alltoall"), (3, "alltoall")])
+def test_gloo_row_shard_merger(world, exchange):
+    """RowShardMerger (preallocated fold sets, one host size sync, absolute-offset
+    imports) over gloo with host-engine sets == the oracle's rank-ordered fold."""
+    S, eps = 40, 0.05
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_merger_worker, args=(r, world, port, S, eps, exchange, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = OracleSet(S, eps)
+    ref.ingest(*shard_data(0, S, eps))
+    for r in range(1, world):
+        o = OracleSet(S, eps)
+        o.ingest(*shard_data(r, S, eps))
+        ref.merge(o)
+    ro, rv, rg, rd = ref.tables()
+    rst = ref.stats()
+    covered = []
+    for rank, (a, b), (to, v, g, d, n, mn, mx) in sorted(results):
+        for k, s in enumerate(range(a, b)):
+            exp = list(zip(rv[ro[s]:ro[s + 1]].tolist(), rg[ro[s]:ro[s + 1]].tolist(), rd[ro[s]:ro[s + 1]].tolist()))
+            got = list(zip(v[to[k]:to[k + 1]], g[to[k]:to[k + 1]], d[to[k]:to[k + 1]]))
+            assert got == exp, (rank, s)
+            assert n[k] == rst["n"][s] and mn[k] == rst["min"][s] and mx[k] == rst["max"][s]
+        covered.extend(range(a, b))
+    assert covered == list(range(S))
