@@ -89,15 +89,26 @@ def make_zipf_input(S, seed, device, cap=10_000_000):
 
 
 def pmc_traffic(workload):
-    """HBM bytes per k_ingest launch measured by PMC counters for this workload
-    (profiles/pmc_traffic.json, written from a committed rocprofv3 --pmc run),
-    or None when no profile of this workload is committed."""
+    """(HBM bytes per k_ingest launch, provenance) from PMC counters of this
+    workload (profiles/pmc_traffic.json, written by scripts/profile_cfg3.sh
+    from a rocprofv3 --pmc run).  The entry is stamped with the sha256 of the
+    library that ran; it is used only when the library loaded now has the same
+    hash (else None: a stale measurement is never reported)."""
+    import hashlib
+    from gkarray_amd import _lib
     p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_traffic.json")
     try:
         with open(p) as f:
-            return json.load(f)[workload]["traffic_bytes"]
+            e = json.load(f)[workload]
     except (OSError, KeyError, ValueError):
-        return None
+        return None, "no PMC profile of this workload"
+    lib = os.environ.get("GK_LIB_PATH") or _lib.LIB_PATH
+    h = hashlib.sha256(open(lib, "rb").read()).hexdigest()
+    if e.get("lib_sha256") != h:
+        return None, "PMC profile was taken on library %s, not this one (%s)" % (
+            str(e.get("lib_sha256"))[:12], h[:12])
+    return e["traffic_bytes"], "PMC (2*FETCH_SIZE + WRITE_SIZE) of this library (sha256 %s), %s" % (
+        h[:12], e.get("source", ""))
 
 
 def algorithmic_bytes(ss, S, N, nq):
@@ -262,6 +273,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
+    traffic, traffic_src = pmc_traffic(a.workload)
     total_values = N * world * a.steps
     value = total_values / dt
     ms_step = dt / a.steps * 1e3
@@ -293,7 +305,8 @@ def main():
                    else ("row-sharded x%d, RCCL %s + merge" % (world, a.exchange) if K == 1 else
                          "row-sharded: %d virtual shards on 1 GPU, merge fold (no exchange)" % K)},
         "roofline": {"bound": "hbm", "kernel": "k_ingest", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(a.workload),
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "bytes_per_launch": bytes_per_launch, "launch_ms": k_ms,
                      "stats_kernel_ms": stats_ms / max(launches, 1)},
     }

@@ -15,5 +15,5 @@ timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_ingest|k_
   -d $D/write -o run -- $ARGS > $D/write.log 2>&1 || exit $?
 timeout -k 10 400 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_WAIT_INST_ANY \
   --kernel-include-regex "k_ingest" --output-format csv -d $D/sq -o run -- $ARGS > $D/sq.log 2>&1 || exit $?
-python3 tools/pmc_summary.py $D 1e9 1e6 $D/summary.json
+python3 tools/pmc_summary.py $D 1e9 1e6 $D/summary.json $D/pmc_traffic.json
 tail -1 $D/bench_trace.log | cut -c1-300

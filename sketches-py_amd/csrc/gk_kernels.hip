@@ -25,6 +25,7 @@
 
 #include "gk_state.h"
 #include "gk_launch.h"
+#include "gk_xor.h"
 
 #define GK_PROF_NSEC 12
 #ifdef GK_PROF
@@ -115,23 +116,41 @@ __device__ __forceinline__ int wave_shr1(int v, int fill) {
   return __builtin_amdgcn_update_dpp(fill, v, DPP_WAVE_SHR1, 0xf, 0xf, false);
 }
 
-__device__ __forceinline__ int64_t wave_incl_scan_i64(int64_t v, int lane) {
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    int64_t t = __shfl_up(v, o, 64);
-    if (lane >= o) v += t;
-  }
+// 64-bit DPP move: both halves through the same control; lanes whose
+// source is masked off or outside the row receive `old`
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ int64_t dpp64(int64_t v, int64_t old) {
+  const int lo = __builtin_amdgcn_update_dpp((int)(uint32_t)(uint64_t)old, (int)(uint32_t)(uint64_t)v, CTRL,
+                                             ROWMASK, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(uint32_t)((uint64_t)old >> 32),
+                                             (int)(uint32_t)((uint64_t)v >> 32), CTRL, ROWMASK, 0xf, false);
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+// inclusive wave64 prefix sum / running max of int64 on DPP (no LDS-pipe
+// instruction: the flush's table traffic bounds the LDS)
+__device__ __forceinline__ int64_t wave_incl_scan_i64(int64_t v, int /*lane*/) {
+  v += dpp64<DPP_ROW_SHR(1), 0xf>(v, 0);
+  v += dpp64<DPP_ROW_SHR(2), 0xf>(v, 0);
+  v += dpp64<DPP_ROW_SHR(4), 0xf>(v, 0);
+  v += dpp64<DPP_ROW_SHR(8), 0xf>(v, 0);
+  v += dpp64<DPP_ROW_BCAST15, 0xa>(v, 0);
+  v += dpp64<DPP_ROW_BCAST31, 0xc>(v, 0);
   return v;
 }
 
-__device__ __forceinline__ int64_t wave_incl_max_i64(int64_t v, int lane) {
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    int64_t t = __shfl_up(v, o, 64);
-    if (lane >= o && t > v) v = t;
-  }
+__device__ __forceinline__ int64_t wave_incl_max_i64(int64_t v, int /*lane*/) {
+  v = max(v, dpp64<DPP_ROW_SHR(1), 0xf>(v, INT64_MIN));
+  v = max(v, dpp64<DPP_ROW_SHR(2), 0xf>(v, INT64_MIN));
+  v = max(v, dpp64<DPP_ROW_SHR(4), 0xf>(v, INT64_MIN));
+  v = max(v, dpp64<DPP_ROW_SHR(8), 0xf>(v, INT64_MIN));
+  v = max(v, dpp64<DPP_ROW_BCAST15, 0xa>(v, INT64_MIN));
+  v = max(v, dpp64<DPP_ROW_BCAST31, 0xc>(v, INT64_MIN));
   return v;
 }
+
+// the value of lane-1 (lane 0: fill)
+__device__ __forceinline__ int64_t wave_shr1_i64(int64_t v, int64_t fill) { return dpp64<DPP_WAVE_SHR1, 0xf>(v, fill); }
 
 __device__ __forceinline__ int wave_sum_i32(int v) {
 #pragma unroll
@@ -1479,7 +1498,7 @@ struct SmallLDS {
   int2 tgd[SMALL_CAP + 2];      // entry (g, d) at i; [j0+K] read as successor
   uint32_t gpk[SMALL_CAP + 4];  // per gap: member count
   int2 gi[SMALL_CAP + 2];       // per gap: (k << 16 | member base << 8 | out base, G + d - 1)
-  double mv[64 * VPL];          // pending values grouped by gap
+  double mv[64 * VPL + GK_SMALL_RANK_MAX];  // pending values grouped by gap, +inf after the last
 #ifdef GK_LDS_PAD
   unsigned char pad[GK_LDS_PAD];  // occupancy experiments only
 #endif
@@ -1542,24 +1561,26 @@ __device__ __forceinline__ void small_put(SmallLDS<VPL>& L, int pos, double v, i
 // One value x (insertion index i) of gap `gap` at rank `rk` inside its gap:
 // gk:93-99 for gap < E, gk:85-92 for the tail.
 // gi[gap].x fields
+// gi[gap].x = m << 24 | k << 16 | member base << 8 | out base (m, k <= 128)
 __device__ __forceinline__ int gi_ob(int x) { return x & 0xff; }
 __device__ __forceinline__ int gi_mb(int x) { return (x >> 8) & 0xff; }
-__device__ __forceinline__ int gi_k(int x) { return x >> 16; }
+__device__ __forceinline__ int gi_k(int x) { return (x >> 16) & 0xff; }
+__device__ __forceinline__ int gi_m(int x) { return (int)((uint32_t)x >> 24); }
 
 // One value x of gap `gap` (its info gi) at rank `rk` inside its gap:
 // gk:93-99 for gap < E, gk:85-92 for the tail.
 template <int VPL>
 __device__ __forceinline__ void small_emit(SmallLDS<VPL>& L, int E, int totm, const CsDiv& cd, double x,
                                            int gap, int2 gi, int rk) {
-  if (gap < E) {
-    const int k = gi_k(gi.x);
-    if (rk >= k) small_put(L, gi_ob(gi.x) + rk - k, x, 1, gi.y);
-  } else {
-    const int m = totm - gi_mb(gi.x);
-    const int q = cd.div(rk);
-    const int rr = rk - q * cd.cs;
-    if (rr == cd.cs - 1 || rk == m - 1) small_put(L, gi_ob(gi.x) + q, x, rr + 1, 0);
-  }
+  (void)totm;
+  // both rules evaluated, one store (no divergent branch per value)
+  const bool in_gap = gap < E;
+  const int k = gi_k(gi.x);
+  const int q = cd.div(rk);
+  const int rr = rk - q * cd.cs;
+  const int pos = gi_ob(gi.x) + (in_gap ? rk - k : q);
+  const bool keep = in_gap ? rk >= k : (rr == cd.cs - 1 || rk == gi_m(gi.x) - 1);
+  if (keep) small_put(L, pos, x, in_gap ? 1 : rr + 1, in_gap ? gi.y : 0);
 }
 
 // ---- in-register sort of 128 doubles, two per lane ------------------------
@@ -1567,14 +1588,15 @@ __device__ __forceinline__ void small_emit(SmallLDS<VPL>& L, int E, int totm, co
 // every compare-exchange keeps the smaller key at the lower position: a merge
 // of two ascending runs of KB/2 starts with a mirror stage (i against
 // i ^ (KB-1)), then half-cleaners (i against i ^ J, J = KB/4 .. 1).  The
-// partner lane comes from ds_swizzle (xor within 32 lanes) or ds_bpermute --
-// LDS-pipe instructions, off the VALU, which bounds this kernel; a stage is
-// one compare and two selects per value.  Equal keys may land in either order
+// partner lane comes from DPP row / quad permutations and the permlane16 /
+// permlane32 swaps (gk_xor.h) -- VALU instructions: the LDS pipe, which the
+// table traffic of the flush keeps ~70% busy (SQ_LDS_IDX_ACTIVE,
+// profiles/r02i_*), stays free; a stage is one compare and two selects per value.  Equal keys may land in either order
 // (callers only use this when equal keys are bit-identical).
 template <int J>
 __device__ __forceinline__ int lane_xor_i32(int v, int lane) {
-  if constexpr (J < 32) return __builtin_amdgcn_ds_swizzle(v, 0x1F | (J << 10));
-  else return __builtin_amdgcn_ds_bpermute((lane ^ J) << 2, v);
+  // DPP / permlane on the VALU (gk_xor.h): the LDS pipe is the flush's bottleneck
+  return lane_xor_dpp<J>(v, lane);
 }
 
 template <int J>
@@ -1824,8 +1846,10 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
     so += v ? (uint32_t)(em[e] - ek[e] + (ekeep[e] ? 1 : 0)) : 0u;
   }
   const int tail_lane = E == 0 ? 0 : (E - 1) / K;
+  int mE_tail = 0;
   if (lane == tail_lane) {
     const int mE = (int)L.gpk[E];
+    mE_tail = mE;
     sm += (uint32_t)mE;
     so += (uint32_t)(cd.cs > 128 ? (mE > 0 ? 1 : 0) : cd.div(mE + cd.cs - 1));
   }
@@ -1842,14 +1866,16 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
     int2 gk[K];
 #pragma unroll
     for (int e = 0; e < K; ++e) {
-      gk[e] = make_int2((ek[e] << 16) | (int)((base >> 8) & 0xff00u) | (int)(base & 0xffu), eG[e] + ed[e] - 1);
+      gk[e] = make_int2((em[e] << 24) | (ek[e] << 16) | (int)((base >> 8) & 0xff00u) | (int)(base & 0xffu),
+                        eG[e] + ed[e] - 1);
       if (j0 + e < E && ekeep[e]) small_put(L, (int)(base & 0xffffu) + em[e] - ek[e], ev[e], eG[e], ed[e]);
       base += (j0 + e < E) ? (((uint32_t)em[e] << 16) | (uint32_t)(em[e] - ek[e] + (ekeep[e] ? 1 : 0))) : 0u;
     }
     *(int4*)&L.gi[j0] = make_int4(gk[0].x, gk[0].y, gk[1].x, gk[1].y);
     if constexpr (K == 4) *(int4*)&L.gi[j0 + 2] = make_int4(gk[2].x, gk[2].y, gk[3].x, gk[3].y);
     // a later store: wins over the block store of the lane owning index E
-    if (lane == tail_lane) L.gi[E] = make_int2((int)((base >> 8) & 0xff00u) | (int)(base & 0xffu), 0);
+    if (lane == tail_lane)
+      L.gi[E] = make_int2((mE_tail << 24) | (int)((base >> 8) & 0xff00u) | (int)(base & 0xffu), 0);
   }
   const int totm = (int)(total >> 16);
   wsync<false>();
@@ -1865,6 +1891,10 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
     // every member (self included: never below itself); they are the ranks
     // iff no gap holds equal values, i.e. iff the rank sum reaches
     // sum m(m-1)/2 -- otherwise an exact pass (ties broken by slot) reruns.
+    // The reads run past a value's own members into the next gaps (whose
+    // values are all above it: gaps partition the value range, and x < v_j
+    // <= every member of gap j+1) and, after the last member, into +inf
+    // padding: no index clamps, no member-count tests in the loop.
     int2 gv[VPL];
     int gb[VPL], mm[VPL], me[VPL];
     int omax = 0;  // this lane's largest member count; the loop runs while any lane needs it
@@ -1872,31 +1902,32 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
 #pragma unroll
     for (int r = 0; r < VPL; ++r) {
       const bool v = lane + 64 * r < cnt;
-      const int gap = xg[r];
-      gv[r] = L.gi[gap];
-      const int ge = gap < E ? gi_mb(L.gi[gap + 1].x) : totm;
+      gv[r] = L.gi[xg[r]];
       gb[r] = gi_mb(gv[r].x);
-      const int m = v ? ge - gb[r] : 0;
+      const int m = v ? gi_m(gv[r].x) : 0;
       dsum += v ? m - 1 : 0;
       mm[r] = m >= 2 ? m : 0;  // a lone member has rank 0
       me[r] = (int)xs[r];
       if (v) L.mv[gb[r] + me[r]] = xv[r];
       omax = max(omax, mm[r]);
     }
+    if (lane < GK_SMALL_RANK_MAX) L.mv[totm + lane] = __longlong_as_double(0x7ff0000000000000LL);
     wsync<false>();
     int rk[VPL];
 #pragma unroll
     for (int r = 0; r < VPL; ++r) rk[r] = 0;
-    for (int u0 = 0; __builtin_amdgcn_ballot_w64(u0 < omax) != 0; u0 += 2) {
-      double y[VPL][2];
+    const double* __restrict__ mvb[VPL];
 #pragma unroll
-      for (int r = 0; r < VPL; ++r)
+    for (int r = 0; r < VPL; ++r) mvb[r] = L.mv + gb[r];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) y[r][h] = L.mv[gb[r] + min(u0 + h, max(mm[r] - 1, 0))];
+    for (int u0 = 0; u0 < GK_SMALL_RANK_MAX; u0 += 2) {
+      if (__builtin_amdgcn_ballot_w64(u0 < omax) == 0) break;
 #pragma unroll
-      for (int r = 0; r < VPL; ++r)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) rk[r] += (u0 + h < mm[r] && y[r][h] < xv[r]) ? 1 : 0;
+      for (int r = 0; r < VPL; ++r) {
+        const double y0 = mvb[r][u0], y1 = mvb[r][u0 + 1];
+        rk[r] += (y0 < xv[r]) ? 1 : 0;
+        rk[r] += (y1 < xv[r]) ? 1 : 0;
+      }
     }
     int rsum = 0;
 #pragma unroll
@@ -2028,8 +2059,7 @@ __device__ __attribute__((noinline)) void small_quantiles(SmallLDS<VPL>& L, int 
       run[e] = m;
     }
     const int64_t pm = wave_incl_max_i64(m, lane);
-    int64_t pex = __shfl_up(pm, 1, 64);
-    if (lane == 0) pex = INT64_MIN;
+    const int64_t pex = wave_shr1_i64(pm, INT64_MIN);
 #pragma unroll
     for (int e = 0; e < K; ++e) run[e] = (j0 + e < E) ? (run[e] > pex ? run[e] : pex) : INT64_MAX;
   }

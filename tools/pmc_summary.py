@@ -70,7 +70,35 @@ def main(d, n_values, streams):
     return out
 
 
+def lib_identity():
+    """sha256 of the HIP library that ran, and of the sources it is built from
+    (the GPU box has no .git: the library file identifies the build)."""
+    import hashlib
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.environ.get("GK_LIB_PATH") or os.path.join(root, "sketches-py_amd", "gkarray_amd", "libgkarray_hip.so")
+    h = hashlib.sha256(open(lib, "rb").read()).hexdigest()
+    src = hashlib.sha256()
+    for f in sorted(glob.glob(os.path.join(root, "sketches-py_amd", "csrc", "*.hip")) +
+                    glob.glob(os.path.join(root, "sketches-py_amd", "csrc", "*.cpp")) +
+                    glob.glob(os.path.join(root, "sketches-py_amd", "csrc", "*.h"))):
+        src.update(open(f, "rb").read())
+    return {"lib_sha256": h, "source_sha256": src.hexdigest()}
+
+
 if __name__ == "__main__":
     res = main(sys.argv[1], float(sys.argv[2]), float(sys.argv[3]))
     if len(sys.argv) > 4:
         json.dump(res, open(sys.argv[4], "w"), indent=1)
+    if len(sys.argv) > 5:
+        # stamped traffic entry for bench.py (profiles/pmc_traffic.json format)
+        ident = lib_identity()
+        entry = {"kernel": "k_ingest_small<2> (with the stats role)",
+                 "traffic_bytes": res["k_ingest"].get("traffic_bytes"),
+                 "fetch_bytes_raw": res["k_ingest"]["fetch_bytes_raw"],
+                 "write_bytes": res["k_ingest"]["write_bytes"], "source": sys.argv[1]}
+        entry.update(ident)
+        doc = ("Per-launch HBM traffic of the dominant kernel, from rocprofv3 --pmc passes "
+               "(scripts/profile_cfg3.sh -> tools/pmc_summary.py): 2*FETCH_SIZE + WRITE_SIZE (gfx950 "
+               "correction, MI355X_MICROARCH.md).  Stamped with the sha256 of the library that ran: "
+               "bench.py reports it as roofline.traffic only when the library it loads has the same hash.")
+        json.dump({"_doc": doc, "cfg3": entry}, open(sys.argv[5], "w"), indent=1)
