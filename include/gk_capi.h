@@ -22,12 +22,22 @@
  *    _sum/_avg chains of streams longer than 16384 values) runs on a stream
  *    the set owns; `stream` is made to wait for it, so every later call
  *    enqueued on `stream` sees the finished state.  The caller keeps input
- *    buffers alive until that work has run (stream order).  gk_merge,
+ *    buffers alive and unchanged until the set's next call or gk_sync: a
+ *    stream that needs a class whose arena has no free slot yet is deferred
+ *    and re-run from them by the host runtime before the next call proceeds.
+ *    gk_merge,
  *    gk_merge_compress, gk_import, gk_save / gk_load and gk_num_promoted
  *    synchronise before returning.
- *  - Asynchronous errors: a stream that outgrows even the largest class (or
- *    finds no free slot in it) keeps its previous state and is reported as
- *    GK_E_OVERFLOW by a later call on the set, at the latest by gk_sync.
+ *  - Limits.  Any eps with int(1/eps)+1 < 2^24 is accepted (the reference:
+ *    any eps); tables grow through capacity classes up to 2^27 entries per
+ *    stream (the last classes are allocated on first use).  One stream may
+ *    hold n values while 2*eps*(n-1) <= 2^30 (5.4e10 values at eps=0.01):
+ *    its tuples' g and delta are int32 (GKRec).
+ *  - Asynchronous errors: a stream that would pass a limit above (or finds no
+ *    memory for its class) is refused: its table, pending values and n keep
+ *    their pre-call state (_min/_max/_sum/_avg, computed beside the tables,
+ *    include the call's values), and GK_E_OVERFLOW is reported by a later
+ *    call on the set, at the latest by gk_sync.
  *  - A set is not thread-safe.  The library owns the set's device state;
  *    callers own their input and output buffers.
  */
@@ -43,10 +53,10 @@ extern "C" {
 #define GK_OK 0
 #define GK_E_ARG (-1)          /* bad argument (size, pointer, NaN quantile ...)   */
 #define GK_E_EPS_MISMATCH (-2) /* merge of sets with different eps: gk:118-119     */
-#define GK_E_OVERFLOW (-3)     /* a stream's table exceeded the largest capacity  */
+#define GK_E_OVERFLOW (-3)     /* a stream passed a limit (table size, count)     */
 #define GK_E_HIP (-4)          /* HIP runtime failure                              */
 #define GK_E_NOMEM (-5)        /* device allocation failed                          */
-#define GK_E_UNSUPPORTED (-6)  /* eps outside the supported range                  */
+#define GK_E_UNSUPPORTED (-6)  /* eps below ~6e-8 (flush period beyond 2^24)       */
 #define GK_E_IO (-7)           /* state file cannot be opened / written            */
 #define GK_E_FORMAT (-8)       /* state file malformed, wrong version or checksum  */
 
@@ -60,8 +70,8 @@ const char* gk_last_error(void);
 
 /* GKArray(eps) for `num_streams` streams (gk:21-29): empty tables, n=0,
  * min=+inf, max=-inf, sum=avg=0.  `device` is the HIP device ordinal.
- * `cap_hint` (0 = default) is the per-stream table capacity of the fast path;
- * streams whose table outgrows it are promoted to a larger class
+ * `cap_hint` (0 = default, < 2^27) is the per-stream table capacity the set
+ * starts with; streams whose table outgrows it are promoted to a larger class
  * automatically. */
 int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device,
               gk_set** out);

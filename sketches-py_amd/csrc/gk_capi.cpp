@@ -42,7 +42,10 @@ int fail(int code, const char* fmt, ...) {
 
 constexpr int kCapSmall = GK_SMALL_CAP;  // LDS class (gk_launch.h)
 constexpr int kCapLarge = 2048;  // LDS class, ~92 KB per wave
-constexpr int kCapHuge = 32768;  // global-workspace class
+constexpr int kCapHuge = 32768;  // global-workspace class (k_ingest)
+constexpr int kCapBig = 1 << 20;  // first unbounded class (k_ingest_big) after kCapHuge
+constexpr int kCapMax = 1 << 27;  // largest class (2 GiB per table)
+constexpr int kPMax = 1 << 24;    // largest flush period (eps >= 6e-8)
 constexpr int64_t kRecipTable = (int64_t)1 << 17;  // entries of st.rtab (1 MiB)
 constexpr int kMaxLdsCap = 2048;
 constexpr int kRounds = GK_MAX_CLASSES + 1;  // overflow lists: launch round 0 + one per promotion level
@@ -67,8 +70,11 @@ struct gk_set {
   // the arenas (st.alloc) ahead of need, from counters read back
   // asynchronously at the end of each call (h_ctr, ev_done).
   int32_t* d_ctr = nullptr;                                  // GK_CTR_WORDS counters
-  int32_t* d_list[GK_MAX_CLASSES] = {nullptr, nullptr, nullptr};
-  int32_t* d_rerun[GK_MAX_CLASSES] = {nullptr, nullptr, nullptr};
+  int32_t* d_list[GK_MAX_CLASSES] = {};
+  int32_t* d_rerun[GK_MAX_CLASSES] = {};
+  // kernel of each class: the unbounded k_ingest_big (classes beyond 32768
+  // entries; every class when P > 1024) or the capacity-class kernels
+  bool big[GK_MAX_CLASSES] = {};
   int32_t* d_defer = nullptr;  // streams whose next class had no free slot (S entries)
   int32_t* h_ctr = nullptr;  // pinned: the counters as of the end of the last call
   hipEvent_t ev_done = nullptr;
@@ -85,13 +91,13 @@ struct gk_set {
   int32_t fatal_seen = 0;  // device FATAL count already reported
   int sticky = GK_OK;      // asynchronous error reported by the next call / gk_sync
   std::string sticky_msg;
-  // global workspace for classes beyond LDS
-  unsigned char* d_ws = nullptr;
-  size_t ws_bytes = 0;
-  int64_t ws_blocks = 0;
+  // global workspace of each class beyond LDS (allocated with its first slots)
+  unsigned char* d_ws[GK_MAX_CLASSES] = {};
+  size_t ws_bytes[GK_MAX_CLASSES] = {};
+  int64_t ws_blocks[GK_MAX_CLASSES] = {};
   // overflow lists of the launch rounds (device); counts in one array
   int32_t* d_ovfc = nullptr;              // kRounds counts
-  int32_t* d_ovfl[kRounds] = {nullptr, nullptr, nullptr, nullptr};
+  int32_t* d_ovfl[kRounds] = {};
   int32_t* h_ovf = nullptr;               // pinned readback of a count (+ list) for merge / import
   int64_t* d_zero_offs = nullptr;  // S+1 zeros: offsets of flush-only launches
   unsigned long long* d_work = nullptr;  // stream hand-out counter of the small-class kernel
@@ -133,20 +139,27 @@ GKPoolDev pool_args(const gk_set* h) {
   return p;
 }
 
-int ensure_ws(gk_set* h) {
-  if (h->d_ws) return GK_OK;
-  const int cap = h->st.cap[h->st.nclass - 1];
-  if (cap <= kMaxLdsCap) return GK_OK;
-  size_t b = std::max(gk_ingest_ws_bytes(cap, h->vpl), gk_merge_lds_bytes(cap, h->st.pmax));
+// Global workspace of class c (ingest and merge share it), for classes beyond
+// LDS; allocated when the class gets its first slots.
+int ensure_ws(gk_set* h, int c) {
+  const int cap = h->st.cap[c];
+  if (h->d_ws[c] || (cap <= kMaxLdsCap && !h->big[c])) return GK_OK;
+  size_t b = std::max(h->big[c] ? gk_big_ws_bytes(cap, h->P) : gk_ingest_ws_bytes(cap, h->vpl),
+                      gk_merge_lds_bytes(cap, h->st.pmax));
   b = (b + 4095) & ~(size_t)4095;
-  // blocks of the global-workspace class: it only holds the rare streams
-  // whose tables outgrow LDS, so a few blocks per 4096 streams
-  int64_t blocks = std::min<int64_t>(gk_num_cu(), std::max<int64_t>(8, h->S / 4096));
-  if (h->st.cap[0] > kMaxLdsCap) blocks = std::min<int64_t>(gk_num_cu(), 256);  // every stream is there
-  if (hipMalloc(&h->d_ws, b * blocks) != hipSuccess)
-    return fail(GK_E_NOMEM, "workspace of %lld x %zu bytes failed", (long long)blocks, b);
-  h->ws_bytes = b;
-  h->ws_blocks = blocks;
+  // class 0 holds every stream: many waves; a larger class only the rare
+  // streams that outgrew the ones below, so a few blocks per 4096 streams.
+  // At most ~2 GiB of workspace per class.
+  const int64_t S = std::max<int64_t>(h->S, 1);
+  int64_t blocks = c == 0 ? std::min<int64_t>(S, (int64_t)gk_num_cu() * 8)
+                          : std::min<int64_t>(gk_num_cu(), std::max<int64_t>(8, S / 4096));
+  blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, ((int64_t)2 << 30) / (int64_t)b));
+  if (hipMalloc(&h->d_ws[c], b * blocks) != hipSuccess) {
+    h->d_ws[c] = nullptr;
+    return fail(GK_E_NOMEM, "class-%d workspace of %lld x %zu bytes failed", c, (long long)blocks, b);
+  }
+  h->ws_bytes[c] = b;
+  h->ws_blocks[c] = blocks;
   return GK_OK;
 }
 
@@ -155,6 +168,7 @@ int ensure_ws(gk_set* h) {
 // share of the streams.
 int64_t initial_slots(const gk_set* h, int c) {
   const int64_t S = std::max<int64_t>(h->S, 1);
+  if (c > 0 && h->st.cap[c] > kCapHuge) return 0;  // unbounded classes: on first use
   if (const char* e = getenv("GK_POOL_SLOTS"))  // tests: force tiny arenas (deferral / growth paths)
     return std::max<int64_t>(1, std::min<int64_t>(S, atoll(e)));
   const int64_t slot_bytes = (int64_t)h->st.cap[c] * (int64_t)sizeof(GKRec);
@@ -169,6 +183,7 @@ int grow_class(gk_set* h, int c, int64_t want, hipStream_t s) {
   want = std::min<int64_t>(want, std::max<int64_t>(h->S, 1));
   if (want <= h->st.alloc[c]) return GK_OK;
   HIP_TRY(hipStreamSynchronize(s));
+  if (ensure_ws(h, c) != GK_OK) return GK_E_NOMEM;
   int32_t used = 0;
   HIP_TRY(hipMemcpy(&used, h->d_ctr + GK_CTR_USED + c, sizeof(int32_t), hipMemcpyDeviceToHost));
   const int64_t keep = std::min<int64_t>(std::max(used, 0), h->st.alloc[c]);
@@ -199,8 +214,9 @@ void poll(gk_set* h, bool block) {
   if (fatal > h->fatal_seen && h->sticky == GK_OK) {
     char buf[256];
     snprintf(buf, sizeof(buf),
-             "%d stream(s) (largest id %d) outgrew every table capacity class (largest %d entries) or found no "
-             "free slot: their values of that call were not added",
+             "%d stream(s) (largest id %d) outgrew every table capacity class (largest %d entries), found no "
+             "free slot, or passed the per-stream count limit 2*eps*(n-1) <= 2^30: their values of that call "
+             "were not added",
              fatal - h->fatal_seen, h->h_ctr[GK_CTR_FATAL + 1], h->st.cap[h->st.nclass - 1]);
     h->sticky = GK_E_OVERFLOW;
     h->sticky_msg = buf;
@@ -211,28 +227,68 @@ void poll(gk_set* h, bool block) {
 int promote_rounds(gk_set* h, const double* x, const int64_t* offs, int force, const GKQuery& q, hipStream_t s);
 int mark_done(gk_set* h, hipStream_t s);
 
+// GK_TRACE=1: the host runtime's slow-path decisions on stderr (debugging)
+bool g_trace = getenv("GK_TRACE") != nullptr;
+#define GK_TR(...)                      \
+  do {                                  \
+    if (g_trace) {                      \
+      fprintf(stderr, "[gk] " __VA_ARGS__); \
+      fputc('\n', stderr);              \
+      fflush(stderr);                   \
+    }                                   \
+  } while (0)
+
+// Grow the arenas for the `count` streams of device list `list`, each moving
+// one class up (deferred ingest streams, import overflows): the target class
+// of each is read back (synchronises), so only the classes they go to grow --
+// the unbounded classes (MiB..GiB per slot) are allocated only when used.
+int grow_targets(gk_set* h, const int32_t* list, int64_t count, hipStream_t s) {
+  if (count <= 0) return GK_OK;
+  std::vector<int32_t> ids(count), cls(std::max<int64_t>(h->S, 1));
+  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(hipMemcpy(ids.data(), list, count * sizeof(int32_t), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(cls.data(), h->st.cls, h->S * sizeof(int32_t), hipMemcpyDeviceToHost));
+  int64_t need[GK_MAX_CLASSES] = {};
+  for (int32_t id : ids) {
+    const int t = cls[id] + 1;
+    if (t < h->st.nclass) ++need[t];
+  }
+  for (int c = 1; c < h->st.nclass; ++c) {
+    if (!need[c]) continue;
+    int32_t used = 0;
+    HIP_TRY(hipMemcpy(&used, h->d_ctr + GK_CTR_USED + c, sizeof(int32_t), hipMemcpyDeviceToHost));
+    int64_t want = (int64_t)used + 2 * need[c];
+    if (h->st.cap[c] <= kCapHuge) want = std::max<int64_t>(want, 2 * (int64_t)h->st.alloc[c]);
+    GK_TR("grow_targets: class %d used %d need %lld -> want %lld", c, used, (long long)need[c], (long long)want);
+    int rc = grow_class(h, c, want, s);
+    if (rc) return rc;
+  }
+  return GK_OK;
+}
+
 // Streams the last call deferred (their next class had no free slot): grow
 // the arenas and run them again, from that call's inputs, before anything
 // else touches the set.
 int replay_deferred(gk_set* h, hipStream_t s) {
-  for (int guard = 0; guard < 8; ++guard) {
+  for (int guard = 0; guard < 2 * GK_MAX_CLASSES + 2; ++guard) {
     const int32_t nd = h->h_ctr[GK_CTR_DEFER];
     if (nd <= 0) return GK_OK;
     h->h_ctr[GK_CTR_DEFER] = 0;
-    for (int c = 1; c < h->st.nclass; ++c) {
-      const int64_t used = h->h_ctr[GK_CTR_USED + c];
-      int rc = grow_class(h, c, std::max<int64_t>(2 * (int64_t)h->st.alloc[c], used + 2 * (int64_t)nd), s);
-      if (rc) return rc;
-    }
+    GK_TR("replay: %d deferred stream(s), round %d", nd, guard);
+    int rc = grow_targets(h, h->d_defer, nd, s);
+    GK_TR("replay: grown rc=%d", rc);
+    if (rc) return rc;
     // the deferred list becomes round 0's overflow list
     HIP_TRY(hipMemsetAsync(h->d_ovfc, 0, kRounds * sizeof(int32_t), s));
     HIP_TRY(hipMemcpyAsync(h->d_ovfl[0], h->d_defer, (size_t)nd * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
     HIP_TRY(hipMemcpyAsync(h->d_ovfc, h->d_ctr + GK_CTR_DEFER, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
     HIP_TRY(hipMemsetAsync(h->d_ctr + GK_CTR_DEFER, 0, sizeof(int32_t), s));
-    int rc = promote_rounds(h, h->last.x, h->last.offs, h->last.force, h->last.q, s);
+    rc = promote_rounds(h, h->last.x, h->last.offs, h->last.force, h->last.q, s);
+    GK_TR("replay: enqueued rc=%d", rc);
     if (!rc) rc = mark_done(h, s);
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(s));
+    GK_TR("replay: done");
     poll(h, true);
   }
   return fail(GK_E_OVERFLOW, "deferred streams could not be placed in a capacity class");
@@ -329,8 +385,13 @@ bool stats_fused(const gk_set* h);
 hipError_t launch_class(gk_set* h, int c, const double* x, const int64_t* offs, const int32_t* list,
                         const int32_t* count_ptr, int r, int force, const GKQuery& q, hipStream_t stream,
                         bool prio = false) {
-  return gk_launch_ingest(h->st.cap[c], h->vpl, h->st, x, offs, list, list ? 0 : h->S, count_ptr, c, force, h->d_ws,
-                          h->ws_bytes, h->ws_blocks, ovf_count(h, r), ovf_list(h, r), q, h->d_work,
+  if (c > 0 && h->st.alloc[c] == 0) return hipSuccess;  // no slot yet: no member
+  if (h->big[c])
+    return gk_launch_ingest_big(h->st.cap[c], h->st, x, offs, list, list ? 0 : h->S, count_ptr, c, force,
+                                h->d_ws[c], h->ws_bytes[c], h->ws_blocks[c], ovf_count(h, r), ovf_list(h, r), q,
+                                h->d_work, h->d_ctr, stream);
+  return gk_launch_ingest(h->st.cap[c], h->vpl, h->st, x, offs, list, list ? 0 : h->S, count_ptr, c, force,
+                          h->d_ws[c], h->ws_bytes[c], h->ws_blocks[c], ovf_count(h, r), ovf_list(h, r), q, h->d_work,
                           prio ? h->d_long_list : nullptr, prio ? h->d_long_count : nullptr,
                           prio && h->ps.ws ? h->ps.ws : nullptr, prio && h->ps.ws ? h->ps.list_ws : nullptr,
                           (prio && c == 0 && stats_fused(h)) ? h->fused_stats : 0, stream);
@@ -384,9 +445,18 @@ int promote_rounds(gk_set* h, const double* x, const int64_t* offs, int force, c
   for (int r = 1; r <= R; ++r) {
     HIP_TRY(hipMemsetAsync(h->d_ctr + GK_CTR_RCNT, 0, GK_MAX_CLASSES * sizeof(int32_t), stream));
     HIP_TRY(gk_launch_promote_dev(h->st, ovf_count(h, r - 1), ovf_list(h, r - 1), -1, pool, stream));
+    if (g_trace) {
+      HIP_TRY(hipStreamSynchronize(stream));
+      GK_TR("round %d: promoted", r);
+    }
     if (r == R) break;  // the last promotion only counts what no class can hold
-    for (int c = r; c < R; ++c)
+    for (int c = r; c < R; ++c) {
       HIP_TRY(launch_class(h, c, x, offs, h->d_rerun[c], h->d_ctr + GK_CTR_RCNT + c, r, force, q, stream));
+      if (g_trace) {
+        HIP_TRY(hipStreamSynchronize(stream));
+        GK_TR("round %d: class %d re-run done", r, c);
+      }
+    }
   }
   return GK_OK;
 }
@@ -439,11 +509,11 @@ int run_merge(gk_set* dst, const MergeArgsHost& base, hipStream_t s) {
     a.ovf_count = ovf_count(dst, level);
     a.ovf_list = ovf_list(dst, level);
     if (cap > kMaxLdsCap) {
-      int rc = ensure_ws(dst);
+      int rc = ensure_ws(dst, level);
       if (rc) return rc;
-      a.ws = dst->d_ws;
-      a.ws_bytes = dst->ws_bytes;
-      a.ws_blocks = dst->ws_blocks;
+      a.ws = dst->d_ws[level];
+      a.ws_bytes = dst->ws_bytes[level];
+      a.ws_blocks = dst->ws_blocks[level];
     } else {
       a.ws = nullptr;
       a.ws_bytes = 0;
@@ -454,8 +524,8 @@ int run_merge(gk_set* dst, const MergeArgsHost& base, hipStream_t s) {
     if (todo < 0) return (int)todo;
     if (todo == 0) return GK_OK;
   }
-  return fail(GK_E_OVERFLOW, "%lld stream(s) exceed %d table entries in merge", (long long)todo,
-              dst->st.cap[dst->st.nclass - 1]);
+  return fail(GK_E_OVERFLOW, "%lld stream(s) exceed %d table entries in merge, or the per-stream count limit "
+              "2*eps*(n-1) <= 2^30", (long long)todo, dst->st.cap[dst->st.nclass - 1]);
 }
 
 }  // namespace
@@ -472,8 +542,29 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
   if (num_streams < 0 || num_streams > INT32_MAX) return fail(GK_E_ARG, "num_streams out of range");
   if (std::isnan(eps) || !(eps > 0.0) || !(eps <= 1.0)) return fail(GK_E_ARG, "eps must be in (0, 1]");
   const double inv = 1.0 / eps;
-  if (inv > 1023.0) return fail(GK_E_UNSUPPORTED, "eps=%g: flush period int(1/eps)+1 > 1024 is not supported", eps);
-  if (cap_hint < 0 || cap_hint > kCapHuge) return fail(GK_E_UNSUPPORTED, "cap_hint %lld out of range", (long long)cap_hint);
+  if (inv >= (double)kPMax)
+    return fail(GK_E_UNSUPPORTED, "eps=%g: flush period int(1/eps)+1 beyond %d is not supported", eps, kPMax);
+  if (cap_hint < 0 || cap_hint >= kCapMax) return fail(GK_E_UNSUPPORTED, "cap_hint %lld out of range", (long long)cap_hint);
+  std::vector<int> caps;
+  std::vector<bool> force_big;
+  if (const char* e = getenv("GK_CAPS")) {  // tests: an explicit ladder, "128,2048,4096b" (b: k_ingest_big)
+    for (const char* t = e; *t;) {
+      char* end = nullptr;
+      const long v = strtol(t, &end, 10);
+      if (end == t) return fail(GK_E_ARG, "GK_CAPS=%s: bad list", e);
+      caps.push_back((int)v);
+      force_big.push_back(*end == 'b');
+      t = end + (*end == 'b');
+      if (*t == ',') ++t;
+    }
+    const double P0 = (double)((int)inv + 1);
+    bool okc = !caps.empty() && (int)caps.size() <= GK_MAX_CLASSES;
+    for (size_t c = 0; okc && c < caps.size(); ++c) {
+      okc = caps[c] >= 64 && caps[c] <= kCapMax && (c == 0 || caps[c] > caps[c - 1]);
+      if (caps[c] == kCapSmall) okc = okc && c == 0 && P0 <= 128;
+    }
+    if (!okc) return fail(GK_E_ARG, "GK_CAPS=%s: increasing capacities in [64, %d], 128 only first", e, kCapMax);
+  }
   int dev_count = 0;
   if (hipGetDeviceCount(&dev_count) != hipSuccess || dev_count <= 0)
     return fail(GK_E_HIP, "no HIP device available");
@@ -485,7 +576,7 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
   h->eps = eps;
   h->P = (int)inv + 1;  // gk:60
   h->device = device;
-  h->vpl = vpl_for(h->P);
+  h->vpl = h->P <= 1024 ? vpl_for(h->P) : 0;  // (registers of the capacity-class kernels)
   if (const char* fs = getenv("GK_FUSED_STATS")) h->fused_stats = std::max(0, std::min(64, atoi(fs)));
   GKState& st = h->st;
   st.S = num_streams;
@@ -494,24 +585,35 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
   st.inv_eps = inv;
   st.P = h->P;
   st.pmax = h->P;
-  // Capacity ladder.  Class 0 (every stream) is the 256-entry LDS class when
+  // Capacity ladder.  Class 0 (every stream) is the 128-entry LDS class when
   // a flush period fits two values per lane (iid tables at eps=0.01 stay at
   // <= ~106 entries); adversarial streams are promoted to 2048
-  // (LDS) and then 32768 (global workspace).
-  if (h->P <= 128 && cap_hint <= kCapSmall) {
-    st.nclass = 3;
-    st.cap[0] = kCapSmall;
-    st.cap[1] = kCapLarge;
-    st.cap[2] = kCapHuge;
-  } else if (cap_hint <= kCapLarge) {
-    st.nclass = 2;
-    st.cap[0] = kCapLarge;
-    st.cap[1] = kCapHuge;
-    st.cap[2] = 0;
-  } else {
-    st.nclass = 1;
-    st.cap[0] = kCapHuge;
-    st.cap[1] = st.cap[2] = 0;
+  // (LDS), 32768 (global workspace) and then the unbounded classes of
+  // k_ingest_big.  With P > 1024 (eps < 1/1023) every class is k_ingest_big:
+  // class 0 of 2P entries (iid tables hold ~P/2..P), then x16 steps.
+  auto pow2_at_least = [](int64_t v) {
+    int64_t c = 1;
+    while (c < v) c <<= 1;
+    return c;
+  };
+  if (caps.empty()) {
+    if (h->P <= 1024) {
+      if (h->P <= 128 && cap_hint <= kCapSmall) caps = {kCapSmall, kCapLarge, kCapHuge, kCapBig};
+      else if (cap_hint <= kCapLarge) caps = {kCapLarge, kCapHuge, kCapBig};
+      else if (cap_hint < kCapHuge) caps = {kCapHuge, kCapBig};
+    }
+    if (caps.empty()) {
+      int64_t c = std::max<int64_t>({4096, pow2_at_least(2 * (int64_t)h->P), pow2_at_least(cap_hint + 1)});
+      for (; (int)caps.size() < GK_MAX_CLASSES && c <= kCapMax; c *= 16) caps.push_back((int)c);
+      if (caps.back() < kCapMax && (int)caps.size() < GK_MAX_CLASSES) caps.push_back(kCapMax);
+    }
+  }
+  st.nclass = (int)caps.size();
+  for (int c = 0; c < GK_MAX_CLASSES; ++c) {
+    st.cap[c] = c < st.nclass ? caps[c] : 0;
+    const bool lds = (st.cap[c] == kCapSmall && c == 0) || st.cap[c] == kCapLarge;
+    h->big[c] = c < st.nclass && (h->P > 1024 || st.cap[c] > kCapHuge || (!force_big.empty() && force_big[c]) ||
+                                  (st.cap[c] <= kMaxLdsCap && !lds));
   }
   const int64_t S = std::max<int64_t>(num_streams, 1);
   bool okm = true;
@@ -543,7 +645,7 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
     okm &= hipMalloc(&h->d_list[c], S * sizeof(int32_t)) == hipSuccess;
     okm &= hipMalloc(&h->d_rerun[c], S * sizeof(int32_t)) == hipSuccess;
     const int64_t n = initial_slots(h, c);
-    okm &= hipMalloc(&st.tab[c], (size_t)n * st.cap[c] * sizeof(GKRec)) == hipSuccess;
+    if (n > 0) okm &= hipMalloc(&st.tab[c], (size_t)n * st.cap[c] * sizeof(GKRec)) == hipSuccess;
     st.alloc[c] = (int32_t)n;
   }
   okm &= hipMalloc(&h->d_zero_offs, (S + 1) * sizeof(int64_t)) == hipSuccess;
@@ -554,7 +656,7 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
   okm &= hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking) == hipSuccess;
   okm &= hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) == hipSuccess;
   okm &= hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) == hipSuccess;
-  if (h->P > 128) {  // class 0 is a capacity-class kernel: presort long streams' batches
+  if (h->P > 128 && !h->big[0]) {  // class 0 is a capacity-class kernel: presort long streams' batches
     okm &= hipMalloc(&h->ps.list_ws, S * sizeof(int64_t)) == hipSuccess;
     okm &= hipMalloc(&h->ps.list_b0, (S + 1) * sizeof(int64_t)) == hipSuccess;
     okm &= hipMalloc(&h->ps.ws_need, sizeof(int64_t)) == hipSuccess;
@@ -565,9 +667,11 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
     gk_destroy(h);
     return fail(GK_E_NOMEM, "device allocation for %lld streams failed", (long long)num_streams);
   }
-  if (ensure_ws(h) != GK_OK) {  // the global-workspace class may be entered inside any call
-    gk_destroy(h);
-    return GK_E_NOMEM;
+  for (int c = 0; c < st.nclass; ++c) {  // classes with slots: their workspace (entered inside any call)
+    if (st.alloc[c] > 0 && ensure_ws(h, c) != GK_OK) {
+      gk_destroy(h);
+      return GK_E_NOMEM;
+    }
   }
   if (hipMemset(st.cls, 0, S * sizeof(int32_t)) != hipSuccess ||
       hipMemset(h->d_ctr, 0, GK_CTR_WORDS * sizeof(int32_t)) != hipSuccess ||
@@ -587,14 +691,17 @@ int gk_destroy(gk_set* h) {
   (void)hipDeviceSynchronize();  // launches of this set may still be running on the caller's stream
   GKState& st = h->st;
   void* ptrs[] = {st.n,       st.E,          st.pend,        st.mn,          st.mx,          st.sum,
-                  st.avg,     st.cls,        st.slot,        st.tab[0],      st.tab[1],      st.tab[2],
-                  st.pbuf,    h->d_list[1],  h->d_list[2],   h->d_rerun[1],  h->d_rerun[2],  h->d_qs,
-                  h->d_ovfc,  h->d_ovfl[0],  h->d_ovfl[1],   h->d_ovfl[2],   h->d_ovfl[3],   h->d_ctr,
-                  h->d_ws,    h->d_zero_offs, h->d_work,     h->d_long_list, h->d_long_n,    h->d_long_count,
+                  st.avg,     st.cls,        st.slot,        st.pbuf,        h->d_qs,        h->d_ovfc,
+                  h->d_ctr,   h->d_zero_offs, h->d_work,     h->d_long_list, h->d_long_n,    h->d_long_count,
                   h->ps.list_ws, h->ps.list_b0, h->ps.ws,    h->ps.ws_need,  st.rtab,        st.n0,
                   h->d_defer};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  for (int c = 0; c < GK_MAX_CLASSES; ++c)
+    for (void* p : {(void*)st.tab[c], (void*)h->d_list[c], (void*)h->d_rerun[c], (void*)h->d_ws[c]})
+      if (p) (void)hipFree(p);
+  for (int r = 0; r < kRounds; ++r)
+    if (h->d_ovfl[r]) (void)hipFree(h->d_ovfl[r]);
   for (auto* v : {&h->tev_flush, &h->tev_stats})
     for (hipEvent_t e : *v) (void)hipEventDestroy(e);
   for (hipEvent_t e : {h->ev_fork, h->ev_join, h->ev_done, h->ev_qs})
@@ -877,10 +984,8 @@ int gk_import(gk_set* h, const int64_t* offs, const double* v, const int32_t* g,
     const int64_t c = read_overflow(h, 0, s);
     if (c < 0) return (int)c;
     if (c == 0) return GK_OK;
-    for (int k = 1; k < h->st.nclass; ++k) {
-      rc = grow_class(h, k, (int64_t)h->st.alloc[k] + c, s);
-      if (rc) return rc;
-    }
+    rc = grow_targets(h, ovf_list(h, 0), c, s);
+    if (rc) return rc;
     HIP_TRY(gk_launch_promote_dev(h->st, ovf_count(h, 0), ovf_list(h, 0), -2, pool, s));
     rc = mark_done(h, s);
     if (!rc) rc = gk_sync(h, stream);

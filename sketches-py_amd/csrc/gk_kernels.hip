@@ -68,9 +68,17 @@ __device__ __forceinline__ GKBigProf& gk_big_prof() {
 
 #define GK_KEEP_BIT 0x40000000
 
-// Largest T handled with int32 arithmetic: T = floor(2 eps (n-1)) is clamped
-// here; it would need n > 2^30/(2 eps) values in ONE stream to matter.
+// Largest T handled in int32 fields: T = floor(2 eps (n-1)) <= 2^30, i.e.
+// n <= 2^29/eps values in ONE stream (5.4e10 at eps = 0.01).  No result is
+// ever computed with a clamped T: the ingest kernels check the stream's count
+// after the call first (gk_count_ok) and refuse a stream that would pass it
+// (overflow -> promotion -> the unbounded class reports it, GK_E_OVERFLOW).
 #define GK_T_CLAMP (1 << 30)
+
+// T of every flush up to count `n_final` fits GK_T_CLAMP
+__device__ __forceinline__ bool gk_count_ok(const GKState& st, int64_t n_final) {
+  return st.two_eps * (double)(n_final - 1) < (double)GK_T_CLAMP + 1.0;
+}
 
 __device__ __forceinline__ int gk_threshold(const GKState& st, int64_t n) {
   // np.floor(2.0*self.eps*(self._n - 1))  (gk:70): (2.0*eps) * float(n-1)
@@ -1335,9 +1343,9 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
     wsync<CAP == 0>();
     GK_BMARK(0);
 
-    // an imported / merged table with no room for the search padding goes
-    // straight to the overflow path (promotion)
-    bool ok = E <= cap - 1;
+    // an imported / merged table with no room for the search padding, or a
+    // stream past the count limit, goes straight to the overflow path
+    bool ok = E <= cap - 1 && gk_count_ok(st, n + (Lx > 0 ? Lx : 0));
     bool flushed = false;  // at least one automatic flush in this call
     int64_t used = 0;
     int64_t need = P - (n % P);  // adds until n hits the next multiple of P (gk:60)
@@ -1451,6 +1459,354 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
   if (lane == 0)
     for (int i = 0; i < GK_PROF_NSEC; ++i) atomicAdd(&gk_prof_acc[i], gk_big_prof().acc[i]);
 #endif
+}
+
+// ===========================================================================
+// k_ingest_big: the add-driven flush (gk:49-109) with no size limit -- the
+// class for tables beyond 32768 entries and, for eps < 1/1023 (flush period
+// P > 1024), every class.  Same stream loop and closed form as k_ingest, but
+// nothing lives in registers or in 16-bit fields: one wave per stream works
+// in a per-block global workspace (BigBuf) of `cap` entries and NP >= P values.
+// Per flush the batch (pending values, then the call's values, in insertion
+// order) is sorted by (value, insertion index) -- Python's stable sorted() of
+// gk:71-72 -- with a wave bitonic sort; A_j = #{values < v_j} splits it into
+// gaps (gap j = sorted positions [A_{j-1}, A_j): gk:93 puts a value equal to an
+// entry after it); then the carry walk and the emit of flush_wave in 32/64-bit
+// arithmetic.  T = floor(2 eps (n-1)) stays exact: a stream whose count would
+// take T past GK_T_CLAMP is refused before any work (GK_CTR_FATAL).
+// ===========================================================================
+struct BigBuf {
+  double* tv[2];
+  int32_t* tg[2];
+  int32_t* td[2];
+  int32_t* ga;    // [cap+1] A_j: sorted values below entry j
+  int32_t* gk;    // [cap+1] absorbed count k | KEEP bit
+  int32_t* gG;    // [cap+1] G, then the delta G + d - 1 of emitted gap values
+  uint32_t* gob;  // [cap+1] first output position of gap j (j == E: the tail)
+  double* mv;     // [NP] the batch: values, sorted in place
+  uint32_t* mi;   //      their insertion index
+};
+
+// sort slots of the batch: a power of two >= 2P (a flush takes p + need <= P
+// values of a consistent state; an imported one may hold up to P-1 pending
+// values more, which must not run past the buffer)
+__host__ __device__ inline int gk_big_np(int P) {
+  int n = 64;
+  while (n < 2 * P) n <<= 1;
+  return n;
+}
+
+__host__ __device__ inline size_t gk_big_ws_bytes_dev(int cap, int P) {
+  const size_t np = (size_t)gk_big_np(P);
+  const size_t b = (2 * (size_t)cap + np) * 8 + (4 * (size_t)cap + 4 * ((size_t)cap + 1) + np) * 4;
+  return (b + 255) & ~(size_t)255;
+}
+
+__device__ inline BigBuf big_buf(unsigned char* base, int cap, int np) {
+  BigBuf b;
+  double* dp = (double*)base;
+  b.tv[0] = dp; dp += cap;
+  b.tv[1] = dp; dp += cap;
+  b.mv = dp; dp += np;
+  int32_t* ip = (int32_t*)dp;
+  b.tg[0] = ip; ip += cap;
+  b.tg[1] = ip; ip += cap;
+  b.td[0] = ip; ip += cap;
+  b.td[1] = ip; ip += cap;
+  b.ga = ip; ip += cap + 1;
+  b.gk = ip; ip += cap + 1;
+  b.gG = ip; ip += cap + 1;
+  b.gob = (uint32_t*)ip; ip += cap + 1;
+  b.mi = (uint32_t*)ip;
+  return b;
+}
+
+// One flush of the `cnt` values in B.mv / B.mi (insertion order) into the
+// table in buffer `cur` (E entries).  Returns the new size (table in buffer
+// cur^1), or -1 if it would exceed cap-1 (nothing written to the table).
+__device__ int big_flush(const BigBuf& B, const int cap, const int cur, const int E, const int cnt, const int T,
+                         const int lane) {
+  const double* __restrict__ tv = cur ? B.tv[1] : B.tv[0];
+  const int32_t* __restrict__ tg = cur ? B.tg[1] : B.tg[0];
+  const int32_t* __restrict__ td = cur ? B.td[1] : B.td[0];
+  double* __restrict__ nv = cur ? B.tv[0] : B.tv[1];
+  int32_t* __restrict__ ng = cur ? B.tg[0] : B.tg[1];
+  int32_t* __restrict__ nd = cur ? B.td[0] : B.td[1];
+  double* __restrict__ mv = B.mv;
+  uint32_t* __restrict__ mi = B.mi;
+
+  // ---- stable order of the batch (gk:71-72) ---------------------------------
+  int N = 1;
+  while (N < cnt) N <<= 1;
+  for (int i = cnt + lane; i < N; i += 64) {
+    mv[i] = __longlong_as_double(0x7ff0000000000000LL);
+    mi[i] = 0xffffffffu;  // after every real value, +inf included
+  }
+  wsync<true>();
+  for (int k = 2; k <= N; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int pp = lane; pp < N / 2; pp += 64) {
+        const int i = ((pp & ~(j - 1)) << 1) | (pp & (j - 1));
+        const int l = i + j;
+        const double a = mv[i], b = mv[l];
+        const uint32_t pa = mi[i], pb = mi[l];
+        const bool a_gt = (a > b) || (a == b && pa > pb);
+        if (a_gt == ((i & k) == 0)) {
+          mv[i] = b;
+          mv[l] = a;
+          mi[i] = pb;
+          mi[l] = pa;
+        }
+      }
+      wsync<true>();
+    }
+  }
+  // ---- gap boundaries: A_j = #{sorted values < v_j} --------------------------
+  for (int j = lane; j < E; j += 64) {
+    const double t = tv[j];
+    int lo = 0, hi = cnt;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (mv[mid] < t) lo = mid + 1;
+      else hi = mid;
+    }
+    B.ga[j] = lo;
+  }
+  wsync<true>();
+  auto gap_m = [&](int j) -> int { return B.ga[j] - (j ? B.ga[j - 1] : 0); };
+
+  // ---- carry walk (closed form of gk:93-106, see flush_wave) -----------------
+  const int K = (E + 63) >> 6;
+  const int j0 = lane * K;
+  const int jend = min(j0 + K, E);
+  const bool has = j0 < E;
+  const int64_t T64 = T;
+  const int cs = T > 1 ? T : 1;
+  const int tail_lane = E == 0 ? 0 : (E - 1) / K;
+  bool known = (lane == 0) || !has;
+  if (has && lane > 0) {
+    const int jp = j0 - 1;
+    const int64_t g = tg[jp], d = td[jp];
+    const int64_t G0 = g + min(max(T64 - d - g, (int64_t)0), (int64_t)gap_m(jp));
+    known = !(G0 + tg[j0] + td[j0] <= T64);
+  }
+  bool done = !has;
+  int64_t cin = 0, cout = 0;
+  for (;;) {
+    if (known && !done) {
+      int64_t c = cin;
+      for (int j = j0; j < jend; ++j) {
+        const int64_t g = tg[j], d = td[j];
+        const int m = gap_m(j);
+        const int64_t Gp = g + c;
+        const int k = (int)min(max(T64 - d - Gp, (int64_t)0), (int64_t)m);
+        const int64_t G = Gp + k;
+        const bool rem = (j + 1 < E) && (G + tg[j + 1] + td[j + 1] <= T64);
+        B.gk[j] = k | (rem ? 0 : GK_KEEP_BIT);
+        B.gG[j] = (int32_t)G;
+        c = rem ? G : 0;
+      }
+      cout = c;
+      done = true;
+    }
+    int64_t pc = __shfl_up(cout, 1, 64);
+    const int pd = wave_shr1((int)done, 1);
+    if (!known && pd) {
+      known = true;
+      cin = pc;
+    }
+    if (__all(done)) break;
+  }
+  // ---- output positions (a wave scan of the per-lane counts), kept entries --
+  uint32_t so = 0;
+  for (int j = j0; j < jend; ++j) {
+    const int kk = B.gk[j];
+    so += (uint32_t)(gap_m(j) - (kk & ~GK_KEEP_BIT) + ((kk & GK_KEEP_BIT) ? 1 : 0));
+  }
+  const int tb = E ? B.ga[E - 1] : 0;  // first sorted position of the tail
+  const int mE = cnt - tb;
+  if (lane == tail_lane) so += (uint32_t)((mE + cs - 1) / cs);
+  const uint32_t incl = wave_incl_scan_u32(so, lane);
+  const int newE = __builtin_amdgcn_readlane((int)incl, 63);
+  if (newE > cap - 1) return -1;  // (uniform)
+  uint32_t base = incl - so;
+  for (int j = j0; j < jend; ++j) {
+    const int m = gap_m(j);
+    const int kk = B.gk[j];
+    const int k = kk & ~GK_KEEP_BIT;
+    const int G = B.gG[j];
+    const int d = td[j];
+    B.gob[j] = base;
+    B.gG[j] = G + d - 1;
+    if (kk & GK_KEEP_BIT) {
+      const uint32_t pos = base + (uint32_t)(m - k);
+      nv[pos] = tv[j];
+      ng[pos] = G;
+      nd[pos] = d;
+    }
+    base += (uint32_t)(m - k + ((kk & GK_KEEP_BIT) ? 1 : 0));
+  }
+  if (lane == tail_lane) B.gob[E] = base;
+  wsync<true>();
+  // ---- the batch values: R3 false branch in the gaps, R2 chunks in the tail --
+  for (int q = lane; q < cnt; q += 64) {
+    const double x = mv[q];
+    int lo = 0, hi = E;  // gap j = #{j' : A_j' <= q}
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (B.ga[mid] <= q) lo = mid + 1;
+      else hi = mid;
+    }
+    const int j = lo;
+    if (j < E) {
+      const int rk = q - (j ? B.ga[j - 1] : 0);
+      const int k = B.gk[j] & ~GK_KEEP_BIT;
+      if (rk >= k) {
+        const uint32_t pos = B.gob[j] + (uint32_t)(rk - k);
+        nv[pos] = x;
+        ng[pos] = 1;
+        nd[pos] = B.gG[j];
+      }
+    } else {
+      const int rk = q - tb;
+      const int qq = rk / cs;
+      const int rr = rk - qq * cs;
+      if (rr == cs - 1 || rk == mE - 1) {
+        const uint32_t pos = B.gob[E] + (uint32_t)qq;
+        nv[pos] = x;
+        ng[pos] = rr + 1;
+        nd[pos] = 0;
+      }
+    }
+  }
+  wsync<true>();
+  return newE;
+}
+
+// The batch of a flush into B.mv / B.mi: p pending values, then c - p values of x.
+__device__ __forceinline__ void big_load(const BigBuf& B, const double* __restrict__ pb, int p,
+                                         const double* __restrict__ xs, int c, int lane) {
+  for (int i = lane; i < c; i += 64) {
+    B.mv[i] = i < p ? pb[i] : xs[i - p];
+    B.mi[i] = (uint32_t)i;
+  }
+  wsync<true>();
+}
+
+// Arguments as k_ingest (CAP == 0); `ctr`: the set's device counters
+// (GK_CTR_FATAL: streams over the per-stream count limit).
+__global__ __launch_bounds__(64) void k_ingest_big(GKState st, const double* __restrict__ x,
+                                                   const int64_t* __restrict__ offs,
+                                                   const int32_t* __restrict__ list, int64_t count,
+                                                   const int32_t* __restrict__ count_ptr, int lcls, int force,
+                                                   int cap, unsigned char* ws, size_t ws_bytes,
+                                                   int32_t* __restrict__ ovf_count, int32_t* __restrict__ ovf_list,
+                                                   const double* __restrict__ qs, int nq,
+                                                   double* __restrict__ qout, int qmode,
+                                                   unsigned long long* __restrict__ work, int32_t* __restrict__ ctr) {
+  const int lane = threadIdx.x;
+  const int P = st.P;
+  const BigBuf B = big_buf(ws + (size_t)blockIdx.x * ws_bytes, cap, gk_big_np(P));
+  if (count_ptr) count = *count_ptr;
+  for (;;) {
+    unsigned long long wv = 0;
+    if (lane == 0) wv = atomicAdd(work, 1ull);
+    const int64_t w = rfl64((int64_t)wv);
+    if (w >= count) break;
+    const int64_t s = list ? (int64_t)list[w] : w;
+    if (__builtin_amdgcn_readfirstlane(st.cls[s]) != lcls) continue;  // in another class
+    int p = __builtin_amdgcn_readfirstlane(st.pend[s]);
+    int E = __builtin_amdgcn_readfirstlane(st.E[s]);
+    int64_t n = rfl64(st.n[s]);
+    const int64_t xo = rfl64(offs[s]);
+    const int64_t Lx = rfl64(offs[s + 1]) - xo;
+    if (Lx <= 0 && !((force == 1 && p > 0) || (force == 2 && n > 0)) && !qs) continue;
+    // a stream past the per-stream count limit is refused like an overflow,
+    // but counted as fatal (no class can take it)
+    const bool over = !gk_count_ok(st, n + (Lx > 0 ? Lx : 0));
+    const double smn = st.mn[s], smx = st.mx[s];
+    GKRec* __restrict__ tab = gk_table_ptr(st, s);
+    double* __restrict__ pb = st.pbuf + s * (int64_t)st.pmax;
+    bool ok = !over && E <= cap - 1;
+    if (ok) {
+      for (int j = lane; j < E; j += 64) {
+        const GKRec rc = tab[j];
+        B.tv[0][j] = rc.v;
+        B.tg[0][j] = rc.g;
+        B.td[0][j] = rc.d;
+      }
+    }
+    wsync<true>();
+    int cur = 0;
+    int64_t used = 0;
+    int64_t need = P - (n % P);  // adds until n hits the next multiple of P (gk:60)
+    while (ok && used + need <= Lx) {
+      big_load(B, pb, p, x + xo + used, p + (int)need, lane);
+      n += need;
+      const int nE = big_flush(B, cap, cur, E, p + (int)need, gk_threshold(st, n), lane);
+      if (nE < 0) {
+        ok = false;
+        break;
+      }
+      E = nE;
+      cur ^= 1;
+      used += need;
+      p = 0;
+      need = P;
+    }
+    if (ok) {
+      const int64_t rem = Lx - used;  // < need: no automatic flush for these
+      if ((force == 1 && p + rem > 0) || force == 2) {
+        big_load(B, pb, p, rem > 0 ? x + xo + used : pb, p + (int)rem, lane);
+        n += rem;
+        const int nE = big_flush(B, cap, cur, E, p + (int)rem, gk_threshold(st, n), lane);
+        if (nE < 0) {
+          ok = false;
+        } else {
+          E = nE;
+          cur ^= 1;
+          p = 0;
+        }
+      } else {
+        for (int64_t i = lane; i < rem; i += 64) pb[p + i] = x[xo + used + i];
+        p += (int)rem;
+        n += rem;
+      }
+    }
+    if (!ok) {
+      // nothing was written back: the stream keeps its pre-call state and is
+      // re-run after promotion to the next capacity class (or, past the count
+      // limit, reported: GK_CTR_FATAL)
+      if (lane == 0) {
+        if (over) {
+          atomicAdd(&ctr[GK_CTR_FATAL], 1);
+          atomicMax(&ctr[GK_CTR_FATAL + 1], (int)s);
+        } else {
+          const int k = atomicAdd(ovf_count, 1);
+          ovf_list[k] = (int32_t)s;
+        }
+      }
+      wsync<true>();
+      continue;
+    }
+    const double* fv = cur ? B.tv[1] : B.tv[0];
+    const int32_t* fg = cur ? B.tg[1] : B.tg[0];
+    const int32_t* fd = cur ? B.td[1] : B.td[0];
+    if (qs) wave_quantiles<1, 1>(fv, fg, fd, E, n, smn, smx, st, qs, nq, qmode, qout + s * (int64_t)nq, lane);
+    for (int j = lane; j < E; j += 64) {
+      GKRec rc;
+      rc.v = fv[j];
+      rc.g = fg[j];
+      rc.d = fd[j];
+      tab[j] = rc;
+    }
+    if (lane == 0) {
+      st.n[s] = n;
+      st.E[s] = E;
+      st.pend[s] = p;
+    }
+    wsync<true>();
+  }
 }
 
 // ===========================================================================
@@ -2285,8 +2641,9 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
     if (Lx <= 0 && !((force == 1 && p > 0) || (force == 2 && n > 0)) && !qs) continue;
     GKRec* __restrict__ tab = gk_table_ptr_cs(st, s, scls, sslot);
     double* __restrict__ pb = st.pbuf + s * (int64_t)st.pmax;
-    // an imported / merged table without room for the padding: promotion
-    bool ok = E <= SMALL_CAP - 1;
+    // an imported / merged table without room for the padding, or a stream
+    // past the count limit: promotion
+    bool ok = E <= SMALL_CAP - 1 && gk_count_ok(st, n + (Lx > 0 ? Lx : 0));
     if (ok) {
       // 16-byte records moved as int4: all loads issued before the first wait
       const int4* __restrict__ t4 = (const int4*)tab;
@@ -2579,7 +2936,7 @@ __global__ __launch_bounds__(64) void k_merge(MergeArgs a) {
         m.rd[c] = a.ed[eo + c];
       }
     }
-    if (E > CAPL) {
+    if (E > CAPL || !gk_count_ok(st, n)) {  // (n: after the merge, gk:149)
       flag_overflow(a.ovf_count, a.ovf_list, s, lane);
       __syncthreads();
       continue;
@@ -3024,6 +3381,24 @@ static hipError_t launch_ingest_small(const GKState& st, const double* x, const 
 }
 
 size_t gk_ingest_ws_bytes(int cap, int vpl) { return gk_flush_ws_bytes(cap, vpl); }
+size_t gk_big_ws_bytes(int cap, int P) { return gk_big_ws_bytes_dev(cap, P); }
+
+hipError_t gk_launch_ingest_big(int cap, const GKState& st, const double* x, const int64_t* offs,
+                                const int32_t* list, int64_t count, const int32_t* count_ptr, int lcls, int force,
+                                unsigned char* ws, size_t ws_bytes, int64_t ws_blocks, int32_t* ovf_count,
+                                int32_t* ovf_list, const GKQuery& q, unsigned long long* work, int32_t* ctr,
+                                hipStream_t stream) {
+  if (count <= 0 && !count_ptr) return hipSuccess;
+  if (!ws || ws_blocks <= 0 || !work || !ctr || ws_bytes < gk_big_ws_bytes_dev(cap, st.P)) return hipErrorInvalidValue;
+  int64_t grid = ws_blocks;
+  if (!count_ptr && grid > count) grid = count;
+  if (grid < 1) grid = 1;
+  hipError_t e = hipMemsetAsync(work, 0, sizeof(unsigned long long), stream);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_ingest_big, dim3((unsigned)grid), dim3(64), 0, stream, st, x, offs, list, count, count_ptr,
+                     lcls, force, cap, ws, ws_bytes, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode, work, ctr);
+  return hipGetLastError();
+}
 
 hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x, const int64_t* offs,
                             const int32_t* list, int64_t count, const int32_t* count_ptr, int lcls, int force,

@@ -40,6 +40,8 @@ struct MergeArgsHost {
 
 int gk_num_cu();
 size_t gk_ingest_ws_bytes(int cap, int vpl);
+// k_ingest_big (any capacity, any flush period): bytes of one block's workspace
+size_t gk_big_ws_bytes(int cap, int P);
 #define GK_WORK_BYTES 1152  // 8 hand-out counters + the stats-role batch counter, one 128-byte line each
 // `work`: GK_WORK_BYTES of device counters of the small-class launch (dynamic stream hand-out).
 // cap GK_SMALL_CAP / 2048: LDS kernels; any other cap: global workspace ws (ws_bytes per block, ws_blocks blocks)
@@ -51,6 +53,15 @@ hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x
                             int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list, const GKQuery& q,
                             unsigned long long* work, const int32_t* prio, const int32_t* prio_count,
                             const double* psort, const int64_t* prio_ws, int fused_stats, hipStream_t stream);
+// The unbounded class (tables beyond 32768 entries; every class when P > 1024):
+// one wave per stream over ws (ws_bytes >= gk_big_ws_bytes(cap, P) per block,
+// ws_blocks blocks); list / count / count_ptr / lcls / force / q as above;
+// ctr: the set's GK_CTR_* counters (GK_CTR_FATAL: per-stream count limit).
+hipError_t gk_launch_ingest_big(int cap, const GKState& st, const double* x, const int64_t* offs,
+                                const int32_t* list, int64_t count, const int32_t* count_ptr, int lcls, int force,
+                                unsigned char* ws, size_t ws_bytes, int64_t ws_blocks, int32_t* ovf_count,
+                                int32_t* ovf_list, const GKQuery& q, unsigned long long* work, int32_t* ctr,
+                                hipStream_t stream);
 // `fused_stats` > 0: the small-class batch launch (x given, no list) also
 // walks the gk:52-59 stats of every stream of at most GK_STATS_LONG values,
 // in that many waves per CU (then requires the lengths-only k_stats before).

@@ -11,7 +11,7 @@ struct GKRec {
   int32_t d;
 };
 
-#define GK_MAX_CLASSES 3
+#define GK_MAX_CLASSES 4
 
 // Per-set device pointers, passed by value to every kernel.
 struct GKState {

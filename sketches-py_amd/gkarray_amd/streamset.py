@@ -134,7 +134,10 @@ class StreamSet:
         asynchronous error of an earlier call (a stream that outgrew every
         table capacity class keeps its previous state: GK_E_OVERFLOW)."""
         with self._ctx():
-            self._check(self._lib.gk_sync(self._h, self._sp()))
+            try:
+                self._check(self._lib.gk_sync(self._h, self._sp()))
+            finally:
+                self._inflight = None  # the last call's inputs are no longer read
 
     def ingest(self, values, offsets, quantiles=None, single=False, sync=True):
         """Batched ``GKArray.add`` (gk:49-61) over all streams.
@@ -157,6 +160,9 @@ class StreamSet:
         if quantiles is None:
             with self._ctx():
                 self._check(self._lib.gk_ingest(self._h, _ptr(v), _ptr(o), self._sp()))
+            # gk_capi.h: the inputs stay valid until the set's next call or
+            # gk_sync (a deferred stream is re-run from them)
+            self._inflight = (v, o)
             if sync:
                 self.sync()
             return None
@@ -168,6 +174,7 @@ class StreamSet:
         with self._ctx():
             self._check(self._lib.gk_ingest_quantiles(self._h, _ptr(v), _ptr(o), arr, nq, _ptr(out), mode,
                                                   self._sp()))
+        self._inflight = (v, o, out)
         if sync:
             self.sync()
         return out[:, :nq]
