@@ -2461,14 +2461,31 @@ __device__ __attribute__((noinline)) void small_quantiles(SmallLDS<VPL>& L, int 
 #ifndef GK_FS_DEPTH
 #define GK_FS_DEPTH 2  // chunks of 8 values in flight per lane
 #endif
-#define GK_SWORK_IDX 128  // the stats batch counter in `work` (after the 8 ingest parts)
+#define GK_SWORK_IDX 128  // the stats batch counters in `work` (after the 8 ingest parts), one per part
+#ifndef GK_FS_LAG_DEFAULT
+#define GK_FS_LAG_DEFAULT 256  // streams the ingest hand-out runs ahead of a stats batch (GK_FS_LAG overrides)
+#endif
+#ifndef GK_FS_SPIN_MAX
+#define GK_FS_SPIN_MAX (1 << 16)  // pacing waits at most this many s_sleeps per batch (no deadlock by construction)
+#endif
 #define GK_QMARK_MIN 0x7ff4000000000001LL  // quantile = _min of the stream (gk:182-183, 220)
 #define GK_QMARK_MAX 0x7ff4000000000002LL  // quantile = _max of the stream (gk:229)
 
+// Part-aligned and paced (pace > 0): a stats wave serves the streams of its
+// own hand-out part (blockIdx % nparts: the XCD whose ingest waves take that
+// part's streams), 64 consecutive streams per batch, and starts a batch only
+// once the part's ingest hand-out has passed its last stream by `lag`
+// streams -- so its reads of the values hit the L2 lines the ingest waves
+// (same XCD, same moment) fetched, instead of reading the batch from HBM a
+// second time.  pace == 0: no waiting (every wave may be a stats wave).
 __device__ __forceinline__ void fused_stats_role(const GKState& st, const double* __restrict__ x,
                                                  const int64_t* __restrict__ offs,
-                                                 unsigned long long* __restrict__ swork, int lane) {
-  const int64_t nb = (st.S + 63) / 64;
+                                                 unsigned long long* __restrict__ work, int part, int nparts,
+                                                 int64_t count, int pace, int lag, int lane) {
+  const int64_t pbeg = count * part / nparts, pend = count * (part + 1) / nparts;
+  const int64_t nb = (pend - pbeg + 63) / 64;
+  unsigned long long* __restrict__ swork = work + GK_SWORK_IDX + 16 * part;
+  unsigned long long* __restrict__ iwork = work + 16 * part;  // the part's ingest hand-out counter
   // refills past a lane's last chunk read this instead (st.rtab: 1 MiB the set
   // owns, 16-byte aligned; the values are never used)
   const double2* __restrict__ dummy = (const double2*)st.rtab;
@@ -2477,8 +2494,17 @@ __device__ __forceinline__ void fused_stats_role(const GKState& st, const double
     if (lane == 0) v = atomicAdd(swork, 1ull);
     const int64_t b = rfl64((int64_t)v);
     if (b >= nb) break;
-    const int64_t s = b * 64 + lane;
-    const bool live = s < st.S;
+    if (pace) {
+      const int64_t want = min((b + 1) * 64 + (int64_t)lag, pend - pbeg);
+      for (int spin = 0; spin < GK_FS_SPIN_MAX; ++spin) {
+        unsigned long long got = 0;
+        if (lane == 0) got = __hip_atomic_load(iwork, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (rfl64((int64_t)got) >= want) break;
+        __builtin_amdgcn_s_sleep(8);
+      }
+    }
+    const int64_t s = pbeg + b * 64 + lane;
+    const bool live = s < pend;
     const int64_t xo = live ? offs[s] : 0;
     int64_t rem = live ? offs[s + 1] - xo : 0;
     if (rem > GK_STATS_LONG) rem = 0;  // k_stats_long's
@@ -2580,11 +2606,11 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
                                                      int32_t* __restrict__ ovf_count, int32_t* __restrict__ ovf_list,
                                                      const double* __restrict__ qs, int nq,
                                                      double* __restrict__ qout, int qmode,
-                                                     unsigned long long* __restrict__ work, int nstat) {
+                                                     unsigned long long* __restrict__ work, int nstat,
+                                                     int fs_pace, int fs_lag) {
   __shared__ __attribute__((aligned(16))) SmallLDS<VPL> L;
   const int lane = threadIdx.x;
   const int P = st.P;
-    if ((int)blockIdx.x < nstat) fused_stats_role(st, x, offs, work + GK_SWORK_IDX, lane);
 #ifdef GK_PROF
   if (lane == 0) {
     for (int i = 0; i < GK_PROF_NSEC; ++i) L.prof[i] = 0;
@@ -2603,6 +2629,7 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
 #endif
   const int nparts = (int)min((unsigned)GK_WORK_PARTS, gridDim.x);  // every part has a wave
   const int part = (int)(blockIdx.x % (unsigned)nparts);
+  if ((int)blockIdx.x < nstat) fused_stats_role(st, x, offs, work, part, nparts, count, fs_pace, fs_lag, lane);
   const int64_t pbeg = count * part / nparts, pend = count * (part + 1) / nparts;
   int64_t cur = 0, cend = 0;
   auto grab = [&]() -> int64_t {
@@ -3371,8 +3398,11 @@ static hipError_t launch_ingest_small(const GKState& st, const double* x, const 
   }
   hipError_t e = hipMemsetAsync(work, 0, GK_WORK_BYTES, stream);
   if (e != hipSuccess) return e;
+  // pacing needs ingest-only waves in every part (stats waves wait for them)
+  const int pace = nstat > 0 && grid >= 4 * (int64_t)nstat && grid >= 8 * GK_WORK_PARTS ? 1 : 0;
+  static const int lag = getenv("GK_FS_LAG") ? atoi(getenv("GK_FS_LAG")) : GK_FS_LAG_DEFAULT;
   hipLaunchKernelGGL((k_ingest_small<VPL>), dim3((unsigned)grid), dim3(64), 0, stream, st, x, offs, list, count,
-                     force, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode, work, nstat);
+                     force, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode, work, nstat, pace, lag);
   if (nstat > 0 && q.qs && q.nq > 0) {
     const int64_t tot = st.S * (int64_t)q.nq;
     hipLaunchKernelGGL(k_qfix, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, st, q.out, q.nq);

@@ -42,7 +42,7 @@ int gk_num_cu();
 size_t gk_ingest_ws_bytes(int cap, int vpl);
 // k_ingest_big (any capacity, any flush period): bytes of one block's workspace
 size_t gk_big_ws_bytes(int cap, int P);
-#define GK_WORK_BYTES 1152  // 8 hand-out counters + the stats-role batch counter, one 128-byte line each
+#define GK_WORK_BYTES 2048  // 8 hand-out counters + 8 stats-role batch counters, one 128-byte line each
 // `work`: GK_WORK_BYTES of device counters of the small-class launch (dynamic stream hand-out).
 // cap GK_SMALL_CAP / 2048: LDS kernels; any other cap: global workspace ws (ws_bytes per block, ws_blocks blocks)
 // list/count (host count) or list/count_ptr (device count): the streams of a class-lcls launch

@@ -62,16 +62,18 @@ def test_fast_class_has_no_scratch(resource_report, small_isa):
     hand-out) adds one more folded value (48 bytes, 11 scratch instructions
     at most); the ingest-only launch measured the same with and without it
     (GK_FUSED_STATS=0 rows of profiles/r01z_ab_fused_stats.txt).
-    The VPL=1 instance (P <= 64) carries 4 more since the DPP lane exchanges
-    (profiles/r02k_dpp_exchanges_sq.txt): one 4-byte reload per flush; the
-    bench's VPL=2 instance keeps the old bound."""
+    The VPL=1 instance (P <= 64) carries more since the DPP lane exchanges
+    (profiles/r02k_dpp_exchanges_sq.txt: one 4-byte reload per flush) and the
+    paced stats role (per-batch reloads of its part bounds,
+    profiles/r02y_stats_pacing_ab.txt); the bench's VPL=2 instance keeps the
+    old bounds."""
     fast = {k: v for k, v in resource_report.items() if k.startswith("_Z14k_ingest_small")}
     assert len(fast) == 2
     for k, v in fast.items():
-        assert v.get("ScratchSize [bytes/lane]", 0) <= 48, (k, v)
+        assert v.get("ScratchSize [bytes/lane]", 0) <= (64 if "smallILi1E" in k else 48), (k, v)
     for name, body in small_isa.items():
         ops = re.findall(r"^\s*(scratch_\w+)", body, re.M)
-        assert len(ops) <= (16 if "smallILi1E" in name else 12), (name, ops)
+        assert len(ops) <= (24 if "smallILi1E" in name else 12), (name, ops)
 
 
 def test_no_inline_asm_memory_ops():
