@@ -94,7 +94,6 @@ def pmc_traffic(workload):
     from a rocprofv3 --pmc run).  The entry is stamped with the sha256 of the
     library that ran; it is used only when the library loaded now has the same
     hash (else None: a stale measurement is never reported)."""
-    import hashlib
     from gkarray_amd import _lib
     p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_traffic.json")
     try:
@@ -102,13 +101,17 @@ def pmc_traffic(workload):
             e = json.load(f)[workload]
     except (OSError, KeyError, ValueError):
         return None, "no PMC profile of this workload"
-    lib = os.environ.get("GK_LIB_PATH") or _lib.LIB_PATH
-    h = hashlib.sha256(open(lib, "rb").read()).hexdigest()
+    h = _lib.library_identity()["sha256"]
     if e.get("lib_sha256") != h:
         return None, "PMC profile was taken on library %s, not this one (%s)" % (
             str(e.get("lib_sha256"))[:12], h[:12])
     return e["traffic_bytes"], "PMC (2*FETCH_SIZE + WRITE_SIZE) of this library (sha256 %s), %s" % (
         h[:12], e.get("source", ""))
+
+
+def _library_identity():
+    from gkarray_amd import _lib
+    return _lib.library_identity()
 
 
 def algorithmic_bytes(ss, S, N, nq):
@@ -309,6 +312,7 @@ def main():
                      "traffic_source": traffic_src,
                      "bytes_per_launch": bytes_per_launch, "launch_ms": k_ms,
                      "stats_kernel_ms": stats_ms / max(launches, 1)},
+        "library": _library_identity(),
     }
     if rank == 0 and world == 1 and not a.no_cpu and a.workload != "cfg4":
         threads = a.cpu_threads or host_cores()[0]

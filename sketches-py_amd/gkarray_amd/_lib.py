@@ -7,6 +7,7 @@ raises ``GKBackendError``.
 """
 import ctypes
 import os
+import sys
 
 __all__ = ["lib", "load", "load_cpu", "GKBackendError", "check", "LIB_PATH", "CPU_LIB_PATH", "SYMBOLS",
            "CPU_SYMBOLS",
@@ -111,8 +112,11 @@ def load(path=None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    # GK_LIB_PATH selects an alternative build (A/B experiments); default in-tree
+    # GK_LIB_PATH selects an alternative build (A/B experiments; reported by
+    # library_identity() and announced on stderr); default in-tree
     p = path or os.environ.get("GK_LIB_PATH") or LIB_PATH
+    if path is None and os.environ.get("GK_LIB_PATH"):
+        sys.stderr.write("gkarray_amd: GK_LIB_PATH override: loading %s\n" % p)
     if not os.path.exists(p):
         raise GKBackendError(GK_E_HIP, "HIP library not built: %s (run __graft_entry__.build())" % p)
     try:
@@ -130,6 +134,17 @@ def load(path=None):
 
 def lib():
     return load()
+
+
+def library_identity():
+    """The HIP library the process uses: path, sha256, and whether GK_LIB_PATH
+    overrides the in-tree build."""
+    import hashlib
+    p = os.environ.get("GK_LIB_PATH") or LIB_PATH
+    with open(p, "rb") as f:
+        h = hashlib.sha256(f.read()).hexdigest()
+    return {"path": os.path.relpath(p, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))),
+            "sha256": h, "override": bool(os.environ.get("GK_LIB_PATH"))}
 
 
 def last_error(handle=None):
