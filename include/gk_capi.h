@@ -173,6 +173,27 @@ int gk_save(gk_set* set, const char* path, void* stream);
 int gk_peek(const char* path, double* eps, int64_t* num_streams);
 int gk_load(gk_set* set, const char* path, void* stream);
 
+/* ---- row-shard exchange ----------------------------------
+ * A set's whole state as one contiguous, self-describing "packed state"
+ * buffer (layout: sketches-py_amd/csrc/gk_pack.h) that any transport moves as
+ * bytes -- rcclAllGather / MPI_Allgather of device buffers, a socket, a file --
+ * and the rank-ordered fold of such buffers: for every stream, the
+ * reference's left fold sk0.merge(sk1).merge(sk2)... (gk:111-154; each merge
+ * flushes `other` first, gk:126/137).  Buffers are device memory on the
+ * set's GPU (host memory for the CPU engine).  All three calls synchronise.
+ *
+ * gk_pack_bytes: size of the set's packed state (read back from the device).
+ * gk_pack:       writes it into `buf` (`bytes` >= gk_pack_bytes; trailing
+ *                bytes untouched, so equal-sized padded buffers work for an
+ *                all-gather).
+ * gk_fold_packed: dst := bufs[0], then dst.merge(bufs[r]) for r = 1..n-1.
+ *                Every buffer must hold dst's stream count and eps
+ *                (GK_E_EPS_MISMATCH otherwise, as gk_merge).  The previous
+ *                state of dst is replaced. */
+int gk_pack_bytes(gk_set* set, int64_t* bytes, void* stream);
+int gk_pack(gk_set* set, void* buf, int64_t bytes, void* stream);
+int gk_fold_packed(gk_set* dst, const void* const* bufs, int nbufs, void* stream);
+
 /* Introspection for tests and benchmarks. */
 int64_t gk_num_streams(const gk_set* set);
 double gk_eps(const gk_set* set);

@@ -27,6 +27,7 @@
 
 #include "gk_cpu.h"
 #include "gk_format.h"
+#include "gk_pack.h"
 
 namespace {
 
@@ -109,6 +110,7 @@ struct gk_set {
   bool timing = false;
   double ingest_ms = 0;
   int64_t launches = 0;
+  gk_set* fold_scratch = nullptr;  // gk_fold_packed (made on first use)
 };
 
 namespace {
@@ -469,6 +471,7 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
 }
 
 int gk_destroy(gk_set* h) {
+  if (h && h->fold_scratch) gk_destroy(h->fold_scratch);
   delete h;
   return GK_OK;
 }
@@ -728,6 +731,51 @@ int gk_load(gk_set* h, const char* path, void* stream) {
 
 int64_t gk_num_streams(const gk_set* h) { return h ? h->S : -1; }
 double gk_eps(const gk_set* h) { return h ? h->eps : 0.0; }
+// ---- packed state (gk_pack.h): host buffers --------------------------------
+namespace {
+struct HostMem {
+  static int to_host(void* host, const void* src, size_t n, void*) {
+    memcpy(host, src, n);
+    return GK_OK;
+  }
+  static int from_host(void* dst, const void* host, size_t n, void*) {
+    memcpy(dst, host, n);
+    return GK_OK;
+  }
+};
+}  // namespace
+
+int gk_pack_bytes(gk_set* h, int64_t* bytes, void* stream) {
+  int rc = check_set(h);
+  if (rc) return rc;
+  if (!bytes) return fail(GK_E_ARG, "bytes is null");
+  std::vector<int32_t> e(std::max<int64_t>(h->S, 1)), p(std::max<int64_t>(h->S, 1));
+  return gkpack::pack_bytes<HostMem>(h, e.data(), p.data(), bytes, stream);
+}
+
+int gk_pack(gk_set* h, void* buf, int64_t bytes, void* stream) {
+  int rc = check_set(h);
+  if (rc) return rc;
+  if (!buf) return fail(GK_E_ARG, "buf is null");
+  std::vector<int32_t> e(std::max<int64_t>(h->S, 1)), p(std::max<int64_t>(h->S, 1));
+  std::string err;
+  rc = gkpack::pack<HostMem>(h, e.data(), p.data(), buf, bytes, stream, err);
+  return (rc && !err.empty()) ? fail(rc, "%s", err.c_str()) : rc;
+}
+
+int gk_fold_packed(gk_set* dst, const void* const* bufs, int nbufs, void* stream) {
+  int rc = check_set(dst);
+  if (rc) return rc;
+  std::string err;
+  auto make = [&](gk_set** out) {
+    const int r = gk_create(dst->S, dst->eps, 0, 0, out);
+    if (!r) (*out)->threads = dst->threads;
+    return r;
+  };
+  rc = gkpack::fold<HostMem>(dst, bufs, nbufs, &dst->fold_scratch, make, stream, err);
+  return (rc && !err.empty()) ? fail(rc, "%s", err.c_str()) : rc;
+}
+
 int gk_flush_period(const gk_set* h) { return h ? (int)std::min<int64_t>(h->P, INT32_MAX) : -1; }
 int gk_capacity(const gk_set* h, int cls) { return (h && cls == 0) ? INT32_MAX : -1; }  // unbounded, one class
 int64_t gk_num_promoted(const gk_set* h) { return h ? 0 : -1; }

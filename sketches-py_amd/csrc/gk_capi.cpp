@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "gk_capi.h"
+#include "gk_pack.h"
 #include "gk_format.h"
 #include "gk_launch.h"
 #include "gk_state.h"
@@ -120,6 +121,8 @@ struct gk_set {
   // eighths of a wave per CU of the small-class batch launch that walk the gk:52-59
   // stats chains first (0: separate k_stats launch); GK_FUSED_STATS overrides
   int fused_stats = 7;
+  // gk_fold_packed: receives the packed states merged into this set (made on first use)
+  gk_set* fold_scratch = nullptr;
   // timing: event pairs recorded around the timed launches, summed at read
   bool timing = false;
   std::vector<hipEvent_t> tev_flush, tev_stats;
@@ -689,6 +692,7 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
 int gk_destroy(gk_set* h) {
   if (!h) return GK_OK;
   (void)hipDeviceSynchronize();  // launches of this set may still be running on the caller's stream
+  if (h->fold_scratch) gk_destroy(h->fold_scratch);
   GKState& st = h->st;
   void* ptrs[] = {st.n,       st.E,          st.pend,        st.mn,          st.mx,          st.sum,
                   st.avg,     st.cls,        st.slot,        st.pbuf,        h->d_qs,        h->d_ovfc,
@@ -1127,6 +1131,57 @@ int gk_load(gk_set* h, const char* path, void* stream) {
   if (rc) return rc;
   if (e != hipSuccess) return fail(GK_E_HIP, "load: %s", hipGetErrorString(e));
   return GK_OK;
+}
+
+// ---- packed state (gk_pack.h): device buffers ------------------------------
+namespace {
+struct DevMem {
+  static int to_host(void* host, const void* src, size_t n, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    if (hipMemcpyAsync(host, src, n, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+      return fail(GK_E_HIP, "packed state: device-to-host copy failed");
+    return GK_OK;
+  }
+  static int from_host(void* dst, const void* host, size_t n, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    if (hipMemcpyAsync(dst, host, n, hipMemcpyHostToDevice, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+      return fail(GK_E_HIP, "packed state: host-to-device copy failed");
+    return GK_OK;
+  }
+};
+}  // namespace
+
+// The size arrays borrow two of the set's S-entry overflow lists (idle
+// outside an ingest call; the calls below synchronise first).
+int gk_pack_bytes(gk_set* h, int64_t* bytes, void* stream) {
+  int rc = check_set(h);
+  if (rc) return rc;
+  if (!bytes) return fail(GK_E_ARG, "bytes is null");
+  rc = gk_sync(h, stream);
+  if (rc) return rc;
+  return gkpack::pack_bytes<DevMem>(h, h->d_ovfl[1], h->d_ovfl[2], bytes, stream);
+}
+
+int gk_pack(gk_set* h, void* buf, int64_t bytes, void* stream) {
+  int rc = check_set(h);
+  if (rc) return rc;
+  if (!buf) return fail(GK_E_ARG, "buf is null");
+  rc = gk_sync(h, stream);
+  if (rc) return rc;
+  std::string err;
+  rc = gkpack::pack<DevMem>(h, h->d_ovfl[1], h->d_ovfl[2], buf, bytes, stream, err);
+  return (rc && !err.empty()) ? fail(rc, "%s", err.c_str()) : rc;
+}
+
+int gk_fold_packed(gk_set* dst, const void* const* bufs, int nbufs, void* stream) {
+  int rc = check_set(dst);
+  if (rc) return rc;
+  rc = gk_sync(dst, stream);
+  if (rc) return rc;
+  std::string err;
+  auto make = [&](gk_set** out) { return gk_create(dst->S, dst->eps, 0, dst->device, out); };
+  rc = gkpack::fold<DevMem>(dst, bufs, nbufs, &dst->fold_scratch, make, stream, err);
+  return (rc && !err.empty()) ? fail(rc, "%s", err.c_str()) : rc;
 }
 
 int64_t gk_num_streams(const gk_set* h) { return h ? h->S : -1; }

@@ -66,6 +66,9 @@ SYMBOLS = {
     "gk_export_pending": (_INT, [_P, _P, _P, _P]),
     "gk_import": (_INT, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "gk_save": (_INT, [_P, ctypes.c_char_p, _P]),
+    "gk_pack_bytes": (_INT, [_P, ctypes.POINTER(_I64), _P]),
+    "gk_pack": (_INT, [_P, _P, _I64, _P]),
+    "gk_fold_packed": (_INT, [_P, ctypes.POINTER(_P), _INT, _P]),
     "gk_peek": (_INT, [ctypes.c_char_p, ctypes.POINTER(_D), ctypes.POINTER(_I64)]),
     "gk_load": (_INT, [_P, ctypes.c_char_p, _P]),
     "gk_num_streams": (_I64, [_P]),

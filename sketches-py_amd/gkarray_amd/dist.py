@@ -19,13 +19,19 @@ Two ways streams meet several GPUs:
 The exchange helpers (``pack_state`` / ``unpack_state`` / ``all_gather_varlen``
 / ``allgather_states`` / ``alltoall_states`` / ``slice_state``) work on tensors of any device, so the
 same code runs over gloo on CPU tensors.
+
+``fold_packed_allgather`` is the same row-shard combine through the C ABI's
+packed states (gk_pack / gk_fold_packed): one contiguous buffer per rank,
+padded to the largest, one all-gather, the rank-ordered fold in the library
+-- the call sequence a non-Python host (cgo / JNI over RCCL or MPI) uses,
+INTEGRATION.md.
 """
 import torch
 import torch.distributed as dist
 
 __all__ = ["stream_range", "balanced_assignment", "pack_state", "unpack_state", "all_gather_varlen",
            "allgather_states", "alltoall_states", "slice_state", "concat_states", "fold_states",
-           "merge_row_shards", "RowShardMerger"]
+           "merge_row_shards", "RowShardMerger", "allgather_packed", "fold_packed_allgather"]
 
 _F64 = ("v", "pv", "min", "max", "sum", "avg")
 _I64 = ("offs", "poffs", "n")
@@ -351,3 +357,25 @@ class RowShardMerger:
                               n=i[2 * m + 2:], g=j[:ek] if ek else torch.zeros(1, dtype=torch.int32, device=dev),
                               d=j[ek:2 * ek] if ek else torch.zeros(1, dtype=torch.int32, device=dev), lo=0, hi=m))
         return views
+
+
+def allgather_packed(ss, group=None):
+    """Every rank's packed state (StreamSet.pack), in rank order: the sizes
+    agree by one all-reduce (max), each rank packs into a zero-padded buffer
+    of that size, one all-gather moves them."""
+    dev = ss.device
+    n = torch.tensor([ss.pack_bytes()], dtype=torch.int64, device=dev)
+    dist.all_reduce(n, op=dist.ReduceOp.MAX, group=group)
+    buf = torch.zeros(int(n.item()), dtype=torch.uint8, device=dev)
+    ss.pack(buf)
+    out = [torch.empty_like(buf) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(out, buf, group=group)
+    return out
+
+
+def fold_packed_allgather(ss, dst, group=None):
+    """dst := rank 0's state, then dst.merge(rank r's state) for r = 1 ..
+    N-1 (gk:111-154) -- every rank gets the whole fold (row shards of the same
+    streams)."""
+    dst.fold_packed(allgather_packed(ss, group))
+    return dst

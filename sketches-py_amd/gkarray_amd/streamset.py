@@ -375,6 +375,39 @@ class StreamSet:
             raise UnequalEpsilonException("Cannot merge two GKArrays with different epsilon values")
         self._check(rc)
 
+    # ---- packed state (gk_pack_bytes / gk_pack / gk_fold_packed) -------------
+    def pack_bytes(self):
+        """Size of this set's packed state (one contiguous buffer: header
+        words, tables, pending values; layout in csrc/gk_pack.h)."""
+        b = ctypes.c_int64(0)
+        with self._ctx():
+            self._check(self._lib.gk_pack_bytes(self._h, ctypes.byref(b), self._sp()))
+        return b.value
+
+    def pack(self, buf=None):
+        """The packed state as a uint8 tensor on the set's device (host for
+        the CPU engine).  ``buf``: a uint8 tensor of at least pack_bytes()
+        bytes to write into (e.g. an equal-sized all-gather slot)."""
+        if buf is None:
+            buf = torch.empty(self.pack_bytes(), dtype=torch.uint8, device=self.device)
+        if buf.dtype != torch.uint8 or not buf.is_contiguous():
+            raise ValueError("buf must be a contiguous uint8 tensor")
+        with self._ctx():
+            self._check(self._lib.gk_pack(self._h, _ptr(buf), buf.numel(), self._sp()))
+        return buf
+
+    def fold_packed(self, bufs):
+        """self := bufs[0], then self.merge(bufs[r]) for r = 1.. (gk:111-154,
+        every stream): the rank-ordered fold of packed states."""
+        bufs = [b if b.device == torch.device(self.device) else b.to(self.device) for b in bufs]
+        arr = (ctypes.c_void_p * max(len(bufs), 1))(*[b.data_ptr() for b in bufs])
+        with self._ctx():
+            rc = self._lib.gk_fold_packed(self._h, arr, len(bufs), self._sp())
+        if rc == L.GK_E_EPS_MISMATCH:
+            from .gkarray import UnequalEpsilonException
+            raise UnequalEpsilonException("Cannot merge two GKArrays with different epsilon values")
+        self._check(rc)
+
     def merge_compress(self, v=None, g=None, d=None, eoffs=None):
         """``merge_compress(entries)`` (gk:63-109) on every stream; stream s
         merges records [eoffs[s], eoffs[s+1]) (sorted by value).  With no

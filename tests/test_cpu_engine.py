@@ -241,3 +241,41 @@ def test_cpu_symbols_match_headers():
     assert all(hasattr(lib, n) for n in names)
     data = open(_lib.CPU_LIB_PATH, "rb").read()
     assert b"gko_" not in data  # independent of the oracle
+
+
+def test_packed_state_round_trip_and_fold():
+    """gk_pack / gk_fold_packed on the host engine: a packed state restores
+    bit-exactly (fold of one buffer), a 3-way fold equals the oracle's left
+    fold, and mismatched eps / stream counts are refused."""
+    from gkarray_amd import StreamSet, UnequalEpsilonException
+    from gkarray_amd._lib import GKBackendError
+    rng = np.random.default_rng(17)
+    eps, S = 0.01, 25
+    sets, oracles = [], []
+    for k in range(3):
+        seqs = [gen(int(rng.integers(0, 8)), int(rng.integers(0, 900)), rng) for _ in range(S)]
+        flat, offs = csr(seqs)
+        ss = StreamSet(S, eps, device=CPU)
+        ss.ingest(torch.from_numpy(flat), torch.from_numpy(offs))
+        o = OracleSet(S, eps)
+        o.ingest(flat, offs)
+        sets.append(ss)
+        oracles.append(o)
+    bufs = [s.pack() for s in sets]
+    assert bufs[0].numel() == sets[0].pack_bytes()
+    one = StreamSet(S, eps, device=CPU)
+    one.fold_packed(bufs[:1])
+    assert_same_state(one, oracles[0], "restored")
+    big = torch.zeros(bufs[1].numel() + 4096, dtype=torch.uint8)  # padded slot
+    sets[1].pack(big)
+    dst = StreamSet(S, eps, device=CPU)
+    dst.fold_packed([bufs[0], big, bufs[2]])
+    oracles[0].merge(oracles[1])
+    oracles[0].merge(oracles[2])
+    assert_same_state(dst, oracles[0], "3-way fold")
+    with pytest.raises(UnequalEpsilonException):
+        StreamSet(S, 0.02, device=CPU).fold_packed(bufs[:1])
+    with pytest.raises(GKBackendError):
+        StreamSet(S + 1, eps, device=CPU).fold_packed(bufs[:1])
+    with pytest.raises(GKBackendError):
+        sets[0].pack(torch.zeros(16, dtype=torch.uint8))

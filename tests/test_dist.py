@@ -237,3 +237,55 @@ def test_gloo_row_shard_merger(world, exchange):
             assert n[k] == rst["n"][s] and mn[k] == rst["min"][s] and mx[k] == rst["max"][s]
         covered.extend(range(a, b))
     assert covered == list(range(S))
+
+
+def _packed_worker(rank, world, port, S, eps, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gkarray_amd import StreamSet
+        flat, offs = shard_data(rank, S, eps)
+        ss = StreamSet(S, eps, device="cpu")
+        ss.ingest(torch.from_numpy(flat), torch.from_numpy(offs))
+        dst = StreamSet(S, eps, device="cpu")
+        gd.fold_packed_allgather(ss, dst)
+        to, v, g, d = dst.tables()
+        st = dst.stats()
+        po, pv = dst.pending()
+        q.put((rank, (to.tolist(), v.tolist(), g.tolist(), d.tolist(), st["n"].tolist(), st["min"].tolist(),
+                      st["max"].tolist(), st["sum"].tolist(), po.tolist(), pv.tolist())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_fold_packed_allgather(world):
+    """The C-ABI exchange (gk_pack -> all-gather of equal-sized padded buffers
+    -> gk_fold_packed) over gloo with host-engine sets: every rank holds the
+    oracle's rank-ordered fold of all shards, tables, header and pending."""
+    S, eps = 30, 0.05
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_packed_worker, args=(r, world, port, S, eps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = OracleSet(S, eps)
+    ref.ingest(*shard_data(0, S, eps))
+    for r in range(1, world):
+        o = OracleSet(S, eps)
+        o.ingest(*shard_data(r, S, eps))
+        ref.merge(o)
+    ro, rv, rg, rd = ref.tables()
+    rst = ref.stats()
+    rpo, rpv = ref.pending()
+    for rank, (to, v, g, d, n, mn, mx, sm, po, pv) in results:
+        assert to == ro.tolist() and v == rv.tolist() and g == rg.tolist() and d == rd.tolist(), rank
+        assert n == rst["n"].tolist() and mn == rst["min"].tolist() and mx == rst["max"].tolist(), rank
+        assert sm == rst["sum"].tolist(), rank
+        assert po == rpo.tolist() and pv == rpv.tolist(), rank

@@ -140,3 +140,43 @@ def test_promotion_arena_exhaustion_defers_and_reruns(gpu_device, monkeypatch, a
     assert_same_state(ss, o, "deferred re-run")
     q = ss.quantiles([0.01, 0.5, 0.99]).cpu().numpy()
     assert_same_quantiles(q, o.quantiles([0.01, 0.5, 0.99]), "deferred q", small_of(o, 0.01))
+
+
+@pytest.mark.parametrize("eps", [0.01, 0.0005])
+def test_packed_states_fold_on_gpu(gpu_device, eps):
+    """gk_pack / gk_fold_packed through the HIP library: a 3-way rank-ordered
+    fold of device packed states == the oracle's left fold (eps = .0005: the
+    unbounded class); a host-engine packed state (same bytes) folds on the GPU."""
+    from gkarray_amd import StreamSet
+    rng = np.random.default_rng(int(7 / eps))
+    S = 60 if eps >= 0.01 else 8
+    P = int(1 / eps) + 1
+    sets, oracles, flats = [], [], []
+    for k in range(3):
+        seqs = [gen(int(d), int(L), rng) for d, L in zip(rng.integers(0, 8, S), rng.integers(0, 5 * P, S))]
+        flat, offs = csr(seqs)
+        ss = _ss(S, eps, gpu_device)
+        ss.ingest(torch.from_numpy(flat), torch.from_numpy(offs))
+        o = OracleSet(S, eps)
+        o.ingest(flat, offs)
+        sets.append(ss)
+        oracles.append(o)
+        flats.append((flat, offs))
+    bufs = [s.pack() for s in sets]
+    assert bufs[0].device.type == "cuda"
+    dst = _ss(S, eps, gpu_device)
+    dst.fold_packed(bufs)
+    oracles[0].merge(oracles[1])
+    oracles[0].merge(oracles[2])
+    assert_same_state(dst, oracles[0], "gpu 3-way fold")
+    q = dst.quantiles([0.5, 0.99]).cpu().numpy()
+    assert_same_quantiles(q, oracles[0].quantiles([0.5, 0.99]), "folded q", small_of(oracles[0], eps))
+    # cross-engine: the host engine's packed bytes, moved to the device
+    h = StreamSet(S, eps, device="cpu")
+    h.ingest(torch.from_numpy(flats[1][0]), torch.from_numpy(flats[1][1]))
+    hb = h.pack()
+    g2 = _ss(S, eps, gpu_device)
+    g2.fold_packed([hb.to(gpu_device)])
+    o1 = OracleSet(S, eps)
+    o1.ingest(*flats[1])
+    assert_same_state(g2, o1, "host-packed on gpu")
