@@ -2857,6 +2857,8 @@ __device__ __forceinline__ void flag_overflow(int32_t* cnt, int32_t* list, int64
   }
 }
 
+#define GK_MERGE_RANK_MAX 256  // pending values ranked by comparison up to this many; bitonic above
+
 template <bool GLOBAL>
 __global__ __launch_bounds__(64) void k_merge(MergeArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -2969,16 +2971,48 @@ __global__ __launch_bounds__(64) void k_merge(MergeArgs a) {
       continue;
     }
     // ---- stable order of self's raw pending values (gk:72) ------------------
-    for (int i = lane; i < p; i += 64) m.ov[i] = pb[i];
-    __syncthreads();
-    for (int i = lane; i < p; i += 64) {
-      const double x = m.ov[i];
-      int rk = 0;
-      for (int t = 0; t < p; ++t) {
-        const double y = m.ov[t];
-        rk += (y < x) || (y == x && t < i);
+    if (p <= GK_MERGE_RANK_MAX) {
+      // few values: each lane ranks its values against all of them
+      for (int i = lane; i < p; i += 64) m.ov[i] = pb[i];
+      __syncthreads();
+      for (int i = lane; i < p; i += 64) {
+        const double x = m.ov[i];
+        int rk = 0;
+        for (int t = 0; t < p; ++t) {
+          const double y = m.ov[t];
+          rk += (y < x) || (y == x && t < i);
+        }
+        m.sp[rk] = x;
       }
-      m.sp[rk] = x;
+    } else {
+      // a large flush period (eps < 1/256): bitonic sort of (value, index)
+      // in the output arrays (free here; cap >= pow2 above p for every class)
+      int N = 1;
+      while (N < p) N <<= 1;
+      for (int i = lane; i < N; i += 64) {
+        m.ov[i] = i < p ? pb[i] : __longlong_as_double(0x7ff0000000000000LL);
+        m.og[i] = i < p ? i : INT32_MAX;
+      }
+      __syncthreads();
+      for (int k = 2; k <= N; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+          for (int pp = lane; pp < N / 2; pp += 64) {
+            const int i = ((pp & ~(j - 1)) << 1) | (pp & (j - 1));
+            const int l = i + j;
+            const double a = m.ov[i], b = m.ov[l];
+            const int ia = m.og[i], ib = m.og[l];
+            const bool a_gt = (a > b) || (a == b && ia > ib);
+            if (a_gt == ((i & k) == 0)) {
+              m.ov[i] = b;
+              m.ov[l] = a;
+              m.og[i] = ib;
+              m.og[l] = ia;
+            }
+          }
+          __syncthreads();
+        }
+      }
+      for (int i = lane; i < p; i += 64) m.sp[i] = m.ov[i];
     }
     __syncthreads();
     // ---- merged incoming list: `self.incoming + entries` sorted stably, so on
