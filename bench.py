@@ -246,8 +246,17 @@ def main():
             return ss.ingest(x, offs, quantiles=qs, sync=False)
 
     # algorithmic bytes of one k_ingest launch (untimed identical step)
-    step()
-    bytes_per_launch = algorithmic_bytes(ss, S, N, len(qs) if a.workload != "cfg4" else 0)
+    timed_sets = [ss]
+    if a.workload == "cfg4" and K > 1:
+        # one shard's ingest launch (before the merges flush the sets)
+        sets[0].reset()
+        sets[0].ingest(shards[0][0], shards[0][1])
+        bytes_per_launch = algorithmic_bytes(sets[0], S, S * L, 0)
+        timed_sets = sets
+        step()
+    else:
+        step()
+        bytes_per_launch = algorithmic_bytes(ss, S, N, len(qs) if a.workload != "cfg4" else 0)
 
     for _ in range(a.warmup):
         step()
@@ -258,8 +267,9 @@ def main():
             import torch.distributed as dist
             dist.barrier()
 
-    ss.timing(True)
-    ss.read_timing()
+    for t_ss in timed_sets:
+        t_ss.timing(True)
+        t_ss.read_timing()
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -268,8 +278,12 @@ def main():
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
-    flush_ms, stats_ms, launches = ss.read_timing()
-    ss.timing(False)
+    flush_ms = stats_ms = 0.0
+    launches = 0
+    for t_ss in timed_sets:  # every shard's ingest launches (cfg4 virtual shards)
+        f_ms, s_ms, n_l = t_ss.read_timing()
+        t_ss.timing(False)
+        flush_ms, stats_ms, launches = flush_ms + f_ms, stats_ms + s_ms, launches + n_l
     if world > 1:
         import torch.distributed as dist
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
