@@ -97,14 +97,15 @@ struct gk_set {
   size_t ws_bytes[GK_MAX_CLASSES] = {};
   int64_t ws_blocks[GK_MAX_CLASSES] = {};
   // overflow lists of the launch rounds (device); counts in one array
-  int32_t* d_ovfc = nullptr;              // kRounds counts
+  int32_t* d_ovfc = nullptr;              // kRounds counts (words of d_ctr)
   int32_t* d_ovfl[kRounds] = {};
   int32_t* h_ovf = nullptr;               // pinned readback of a count (+ list) for merge / import
   int64_t* d_zero_offs = nullptr;  // S+1 zeros: offsets of flush-only launches
-  unsigned long long* d_work = nullptr;  // stream hand-out counter of the small-class kernel
+  unsigned long long* d_work = nullptr;  // the call's hand-out counters (bytes of d_ctr from GK_CALL_WORK)
+  int next_work = 0;                     // next free 128-byte counter of this call
   int32_t* d_long_list = nullptr;        // streams k_stats hands to k_stats_long (longest first)
   int64_t* d_long_n = nullptr;           //   and their pre-call n
-  int32_t* d_long_count = nullptr;
+  int32_t* d_long_count = nullptr;       // (a word of d_ctr)
   // k_stats_long (the sequential _sum/_avg chains of long streams) runs on
   // this stream beside the ingest launches; ev_fork / ev_join order it
   hipStream_t aux = nullptr;
@@ -134,6 +135,7 @@ namespace {
 GKPoolDev pool_args(const gk_set* h) {
   GKPoolDev p;
   p.ctr = h->d_ctr;
+  p.rcnt = h->d_ctr + GK_CTR_RCNT;
   p.defer = h->d_defer;
   for (int c = 0; c < GK_MAX_CLASSES; ++c) {
     p.list[c] = h->d_list[c];
@@ -230,6 +232,23 @@ void poll(gk_set* h, bool block) {
 int promote_rounds(gk_set* h, const double* x, const int64_t* offs, int force, const GKQuery& q, hipStream_t s);
 int mark_done(gk_set* h, hipStream_t s);
 
+// Start of a call's device work: ONE memset zeroes every per-call counter
+// (deferred / long-stream counts, re-run and overflow list lengths, the
+// launches' stream hand-out counters; gk_launch.h GK_CTR_*).
+int begin_call(gk_set* h, hipStream_t s) {
+  HIP_TRY(hipMemsetAsync(h->d_ctr + GK_CTR_CALL, 0, GK_CALL_BYTES - GK_CTR_CALL * sizeof(int32_t), s));
+  h->next_work = 0;
+  return GK_OK;
+}
+
+// The zeroed hand-out counter of the call's next launch (the small-class
+// launch has its own GK_WORK_BYTES block).
+unsigned long long* work_counter(gk_set* h, bool small) {
+  if (small) return h->d_work;
+  if (h->next_work >= GK_CALL_SLOTS) return nullptr;  // (launches per call are bounded: 1 + R-1 + R(R-1)/2)
+  return (unsigned long long*)((char*)h->d_work + GK_WORK_BYTES + 128 * (h->next_work++));
+}
+
 // GK_TRACE=1: the host runtime's slow-path decisions on stderr (debugging)
 bool g_trace = getenv("GK_TRACE") != nullptr;
 #define GK_TR(...)                      \
@@ -281,11 +300,12 @@ int replay_deferred(gk_set* h, hipStream_t s) {
     int rc = grow_targets(h, h->d_defer, nd, s);
     GK_TR("replay: grown rc=%d", rc);
     if (rc) return rc;
-    // the deferred list becomes round 0's overflow list
-    HIP_TRY(hipMemsetAsync(h->d_ovfc, 0, kRounds * sizeof(int32_t), s));
+    // the deferred list becomes round 0's overflow list of a fresh call
     HIP_TRY(hipMemcpyAsync(h->d_ovfl[0], h->d_defer, (size_t)nd * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
-    HIP_TRY(hipMemcpyAsync(h->d_ovfc, h->d_ctr + GK_CTR_DEFER, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
-    HIP_TRY(hipMemsetAsync(h->d_ctr + GK_CTR_DEFER, 0, sizeof(int32_t), s));
+    int rb = begin_call(h, s);
+    if (rb) return rb;
+    h->h_ovf[0] = nd;  // pinned; the stream is synchronised below before it is reused
+    HIP_TRY(hipMemcpyAsync(h->d_ovfc, h->h_ovf, sizeof(int32_t), hipMemcpyHostToDevice, s));
     rc = promote_rounds(h, h->last.x, h->last.offs, h->last.force, h->last.q, s);
     GK_TR("replay: enqueued rc=%d", rc);
     if (!rc) rc = mark_done(h, s);
@@ -389,12 +409,14 @@ hipError_t launch_class(gk_set* h, int c, const double* x, const int64_t* offs, 
                         const int32_t* count_ptr, int r, int force, const GKQuery& q, hipStream_t stream,
                         bool prio = false) {
   if (c > 0 && h->st.alloc[c] == 0) return hipSuccess;  // no slot yet: no member
+  unsigned long long* work = work_counter(h, c == 0 && h->st.cap[0] == GK_SMALL_CAP && !h->big[0]);
+  if (!work) return hipErrorInvalidValue;
   if (h->big[c])
     return gk_launch_ingest_big(h->st.cap[c], h->st, x, offs, list, list ? 0 : h->S, count_ptr, c, force,
                                 h->d_ws[c], h->ws_bytes[c], h->ws_blocks[c], ovf_count(h, r), ovf_list(h, r), q,
-                                h->d_work, h->d_ctr, stream);
+                                work, h->d_ctr, stream);
   return gk_launch_ingest(h->st.cap[c], h->vpl, h->st, x, offs, list, list ? 0 : h->S, count_ptr, c, force,
-                          h->d_ws[c], h->ws_bytes[c], h->ws_blocks[c], ovf_count(h, r), ovf_list(h, r), q, h->d_work,
+                          h->d_ws[c], h->ws_bytes[c], h->ws_blocks[c], ovf_count(h, r), ovf_list(h, r), q, work,
                           prio ? h->d_long_list : nullptr, prio ? h->d_long_count : nullptr,
                           prio && h->ps.ws ? h->ps.ws : nullptr, prio && h->ps.ws ? h->ps.list_ws : nullptr,
                           (prio && c == 0 && stats_fused(h)) ? h->fused_stats : 0, stream);
@@ -444,9 +466,10 @@ int stats_join(gk_set* h, hipStream_t s, const GKQuery& q) {
 // on the device and runs again in its new class (round r).
 int promote_rounds(gk_set* h, const double* x, const int64_t* offs, int force, const GKQuery& q, hipStream_t stream) {
   const int R = h->st.nclass;
-  const GKPoolDev pool = pool_args(h);
+  GKPoolDev pool = pool_args(h);
   for (int r = 1; r <= R; ++r) {
-    HIP_TRY(hipMemsetAsync(h->d_ctr + GK_CTR_RCNT, 0, GK_MAX_CLASSES * sizeof(int32_t), stream));
+    int32_t* rcnt = h->d_ctr + GK_CTR_RCNT + GK_MAX_CLASSES * r;  // zeroed at the start of the call
+    pool.rcnt = rcnt;
     HIP_TRY(gk_launch_promote_dev(h->st, ovf_count(h, r - 1), ovf_list(h, r - 1), -1, pool, stream));
     if (g_trace) {
       HIP_TRY(hipStreamSynchronize(stream));
@@ -454,7 +477,7 @@ int promote_rounds(gk_set* h, const double* x, const int64_t* offs, int force, c
     }
     if (r == R) break;  // the last promotion only counts what no class can hold
     for (int c = r; c < R; ++c) {
-      HIP_TRY(launch_class(h, c, x, offs, h->d_rerun[c], h->d_ctr + GK_CTR_RCNT + c, r, force, q, stream));
+      HIP_TRY(launch_class(h, c, x, offs, h->d_rerun[c], rcnt + c, r, force, q, stream));
       if (g_trace) {
         HIP_TRY(hipStreamSynchronize(stream));
         GK_TR("round %d: class %d re-run done", r, c);
@@ -474,8 +497,7 @@ int run_ingest(gk_set* h, const double* x, const int64_t* offs, int force, hipSt
   h->last.q = q;
   h->last.may_defer = false;
   for (int c = 1; c < R; ++c) h->last.may_defer |= h->st.alloc[c] < h->S;
-  HIP_TRY(hipMemsetAsync(h->d_ovfc, 0, kRounds * sizeof(int32_t), stream));
-  HIP_TRY(hipMemsetAsync(h->d_ctr + GK_CTR_DEFER, 0, sizeof(int32_t), stream));
+  // (the call's counters were zeroed by begin_call)
   // timing covers the class-0 batch launch of gk_ingest (x given) only
   const bool timed = h->timing && x != nullptr;
   hipEvent_t t0 = timed ? timing_event(h->tev_flush, h->n_flush) : nullptr;
@@ -634,10 +656,15 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
   st.rtab_n = kRecipTable;
   okm &= hipMalloc(&st.rtab, (size_t)st.rtab_n * sizeof(double)) == hipSuccess;
   okm &= hipMalloc(&st.n0, S * sizeof(int64_t)) == hipSuccess;
-  okm &= hipMalloc(&h->d_ovfc, kRounds * sizeof(int32_t)) == hipSuccess;
+
   for (int r = 0; r < kRounds; ++r) okm &= hipMalloc(&h->d_ovfl[r], S * sizeof(int32_t)) == hipSuccess;
   okm &= hipHostMalloc(&h->h_ovf, 16 * sizeof(int32_t)) == hipSuccess;
-  okm &= hipMalloc(&h->d_ctr, GK_CTR_WORDS * sizeof(int32_t)) == hipSuccess;
+  okm &= hipMalloc(&h->d_ctr, GK_CALL_BYTES) == hipSuccess;
+  if (h->d_ctr) {
+    h->d_ovfc = h->d_ctr + GK_CTR_OVFC;
+    h->d_long_count = h->d_ctr + GK_CTR_LONG;
+    h->d_work = (unsigned long long*)((char*)h->d_ctr + GK_CALL_WORK);
+  }
   okm &= hipHostMalloc(&h->h_ctr, GK_CTR_WORDS * sizeof(int32_t)) == hipSuccess;
   okm &= hipMalloc(&h->d_defer, S * sizeof(int32_t)) == hipSuccess;
   if (h->h_ctr) memset(h->h_ctr, 0, GK_CTR_WORDS * sizeof(int32_t));
@@ -652,10 +679,10 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
     st.alloc[c] = (int32_t)n;
   }
   okm &= hipMalloc(&h->d_zero_offs, (S + 1) * sizeof(int64_t)) == hipSuccess;
-  okm &= hipMalloc(&h->d_work, GK_WORK_BYTES) == hipSuccess;
+
   okm &= hipMalloc(&h->d_long_list, S * sizeof(int32_t)) == hipSuccess;
   okm &= hipMalloc(&h->d_long_n, S * sizeof(int64_t)) == hipSuccess;
-  okm &= hipMalloc(&h->d_long_count, sizeof(int32_t)) == hipSuccess;
+
   okm &= hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking) == hipSuccess;
   okm &= hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) == hipSuccess;
   okm &= hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) == hipSuccess;
@@ -677,7 +704,7 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
     }
   }
   if (hipMemset(st.cls, 0, S * sizeof(int32_t)) != hipSuccess ||
-      hipMemset(h->d_ctr, 0, GK_CTR_WORDS * sizeof(int32_t)) != hipSuccess ||
+      hipMemset(h->d_ctr, 0, GK_CALL_BYTES) != hipSuccess ||
       hipMemset(h->d_zero_offs, 0, (S + 1) * sizeof(int64_t)) != hipSuccess ||
       hipMemset(st.slot, 0, S * sizeof(int32_t)) != hipSuccess || gk_launch_reset(st, nullptr) != hipSuccess ||
       gk_launch_rtab(st, nullptr) != hipSuccess ||
@@ -695,8 +722,8 @@ int gk_destroy(gk_set* h) {
   if (h->fold_scratch) gk_destroy(h->fold_scratch);
   GKState& st = h->st;
   void* ptrs[] = {st.n,       st.E,          st.pend,        st.mn,          st.mx,          st.sum,
-                  st.avg,     st.cls,        st.slot,        st.pbuf,        h->d_qs,        h->d_ovfc,
-                  h->d_ctr,   h->d_zero_offs, h->d_work,     h->d_long_list, h->d_long_n,    h->d_long_count,
+                  st.avg,     st.cls,        st.slot,        st.pbuf,        h->d_qs,
+                  h->d_ctr,   h->d_zero_offs, h->d_long_list, h->d_long_n,
                   h->ps.list_ws, h->ps.list_b0, h->ps.ws,    h->ps.ws_need,  st.rtab,        st.n0,
                   h->d_defer};
   for (void* p : ptrs)
@@ -721,11 +748,9 @@ int gk_reset(gk_set* h, void* stream) {
   int rc = check_set(h);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
-  const int64_t S = std::max<int64_t>(h->S, 1);
   rc = settle(h, s, false);  // a deferred re-run of the last call must not land after the reset
   if (rc) return rc;
-  HIP_TRY(hipMemsetAsync(h->st.cls, 0, S * sizeof(int32_t), s));
-  HIP_TRY(hipMemsetAsync(h->st.slot, 0, S * sizeof(int32_t), s));
+  // (k_reset puts every stream back in class 0: cls = slot = 0)
   // slots, member lists and re-run lists start over (FATAL stays cumulative:
   // a readback still in flight carries it)
   HIP_TRY(hipMemsetAsync(h->d_ctr, 0, GK_CTR_FATAL * sizeof(int32_t), s));
@@ -742,6 +767,7 @@ int gk_ingest(gk_set* h, const double* values, const int64_t* offsets, void* str
   hipStream_t s = (hipStream_t)stream;
   rc = grow_pools(h, s);
   if (!rc) rc = take_sticky(h);
+  if (!rc) rc = begin_call(h, s);
   if (rc) return rc;
   rc = stats_fork(h, values, offsets, s);
   if (rc) return rc;
@@ -758,6 +784,7 @@ int gk_flush(gk_set* h, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   rc = grow_pools(h, s);
   if (!rc) rc = take_sticky(h);
+  if (!rc) rc = begin_call(h, s);
   if (rc) return rc;
   rc = run_ingest(h, nullptr, nullptr, 1, s);
   const int rd = mark_done(h, s);
@@ -824,6 +851,7 @@ int gk_quantiles(gk_set* h, const double* qs, int nq, double* out, int mode, voi
   if (nq == 0 || h->S == 0) return GK_OK;
   rc = grow_pools(h, s);
   if (!rc) rc = take_sticky(h);
+  if (!rc) rc = begin_call(h, s);
   if (rc) return rc;
   // gk:197-198: pending values are flushed first (state mutation); the
   // quantiles are answered in the same launch from the flushed table
@@ -846,6 +874,7 @@ int gk_ingest_quantiles(gk_set* h, const double* values, const int64_t* offsets,
   if (nq == 0) return gk_ingest(h, values, offsets, stream);
   rc = grow_pools(h, s);
   if (!rc) rc = take_sticky(h);
+  if (!rc) rc = begin_call(h, s);
   if (rc) return rc;
   rc = stats_fork(h, values, offsets, s);
   if (rc) return rc;
@@ -894,7 +923,8 @@ int gk_merge(gk_set* dst, gk_set* const* srcs, int nsrcs, void* stream) {
     rc = gk_sync(src, stream);
     if (rc) return rc;
     // other.merge_compress() -- unconditional in the reference (gk:126, 137)
-    rc = run_ingest(src, nullptr, nullptr, 2, s);
+    rc = begin_call(src, s);
+    if (!rc) rc = run_ingest(src, nullptr, nullptr, 2, s);
     if (!rc) rc = mark_done(src, s);
     if (!rc) rc = gk_sync(src, stream);
     if (rc) return rc;

@@ -3198,6 +3198,8 @@ __global__ void k_reset(GKState st) {
   st.mx[s] = __longlong_as_double((long long)0xfff0000000000000ULL);  // -inf (gk:26)
   st.sum[s] = 0.0;
   st.avg[s] = 0.0;
+  st.cls[s] = 0;  // every stream back in class 0
+  st.slot[s] = 0;
 }
 
 __global__ void k_export(GKState st, const int64_t* __restrict__ offs, double* __restrict__ v,
@@ -3335,7 +3337,7 @@ __global__ void k_promote_dev(GKState st, const int32_t* __restrict__ count, con
       st.cls[s] = t;
       st.slot[s] = slot;
       pool.list[t][atomicAdd(&pool.ctr[GK_CTR_LCNT + t], 1)] = (int32_t)s;
-      if (level == -1) pool.rerun[t][atomicAdd(&pool.ctr[GK_CTR_RCNT + t], 1)] = (int32_t)s;
+      if (level == -1) pool.rerun[t][atomicAdd(&pool.rcnt[t], 1)] = (int32_t)s;
     }
   }
 }
@@ -3380,8 +3382,6 @@ static hipError_t launch_ingest_t(const GKState& st, const double* x, const int6
   }
   if (!prio && !count_ptr && grid > count) grid = count;
   if (grid < 1) grid = 1;
-  hipError_t e = hipMemsetAsync(work, 0, sizeof(unsigned long long), stream);
-  if (e != hipSuccess) return e;
   hipLaunchKernelGGL((k_ingest<CAP, VPL>), dim3((unsigned)grid), dim3(64), 0, stream, st, x, offs, list,
                      count, count_ptr, lcls, force, cap, ws, ws_bytes, ovf_count, ovf_list, q.qs, q.nq, q.out,
                      q.mode, work, prio, prio_count, psort, prio_ws);
@@ -3430,8 +3430,6 @@ static hipError_t launch_ingest_small(const GKState& st, const double* x, const 
     const int64_t want = std::max<int64_t>(1, (int64_t)num_cu() * fused_stats / 8);  // eighths of a wave per CU
     nstat = (int)(grid < want ? grid : want);
   }
-  hipError_t e = hipMemsetAsync(work, 0, GK_WORK_BYTES, stream);
-  if (e != hipSuccess) return e;
   // pacing needs ingest-only waves in every part (stats waves wait for them)
   const int pace = nstat > 0 && grid >= 4 * (int64_t)nstat && grid >= 8 * GK_WORK_PARTS ? 1 : 0;
   static const int lag = getenv("GK_FS_LAG") ? atoi(getenv("GK_FS_LAG")) : GK_FS_LAG_DEFAULT;
@@ -3457,8 +3455,6 @@ hipError_t gk_launch_ingest_big(int cap, const GKState& st, const double* x, con
   int64_t grid = ws_blocks;
   if (!count_ptr && grid > count) grid = count;
   if (grid < 1) grid = 1;
-  hipError_t e = hipMemsetAsync(work, 0, sizeof(unsigned long long), stream);
-  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_ingest_big, dim3((unsigned)grid), dim3(64), 0, stream, st, x, offs, list, count, count_ptr,
                      lcls, force, cap, ws, ws_bytes, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode, work, ctr);
   return hipGetLastError();
@@ -3492,8 +3488,6 @@ hipError_t gk_launch_stats(const GKState& st, const double* x, const int64_t* of
                            int64_t* long_n, int32_t* long_count, const GKPresort& ps, int lengths_only,
                            hipStream_t stream) {
   if (st.S <= 0) return hipSuccess;
-  hipError_t e = hipMemsetAsync(long_count, 0, sizeof(int32_t), stream);
-  if (e != hipSuccess) return e;
   const int64_t grid = (st.S + 255) / 256;
   hipLaunchKernelGGL(k_stats, dim3((unsigned)grid), dim3(256), 0, stream, st, x, offs, long_list, long_count,
                      lengths_only);

@@ -43,7 +43,9 @@ size_t gk_ingest_ws_bytes(int cap, int vpl);
 // k_ingest_big (any capacity, any flush period): bytes of one block's workspace
 size_t gk_big_ws_bytes(int cap, int P);
 #define GK_WORK_BYTES 2048  // 8 hand-out counters + 8 stats-role batch counters, one 128-byte line each
-// `work`: GK_WORK_BYTES of device counters of the small-class launch (dynamic stream hand-out).
+// `work`: device counters of the launch's dynamic stream hand-out, ZEROED BY THE CALLER
+// (GK_WORK_BYTES for the small-class launch, 8 bytes for the others; gk_capi.cpp
+// zeroes every counter of a call with one memset, GK_CALL_* below).
 // cap GK_SMALL_CAP / 2048: LDS kernels; any other cap: global workspace ws (ws_bytes per block, ws_blocks blocks)
 // list/count (host count) or list/count_ptr (device count): the streams of a class-lcls launch
 // (list NULL: every stream, class 0); listed streams no longer in class lcls are skipped.
@@ -112,14 +114,30 @@ hipError_t gk_launch_promote(const GKState& st, const int32_t* list, int64_t cou
 // Device-side capacity-class bookkeeping: counters (slots used, member list
 // lengths, re-run list lengths, streams that found no class / slot) and, per
 // class c > 0, its member list and this round's re-run list (S entries each).
+// Layout of the set's counter block (int32 words; one allocation):
+//   persistent:  [0..3] slots used per class, [4..7] member-list lengths,
+//                [12] streams with no class left, [13] the largest such id
+//   per call (zeroed by ONE memset at the start of every call, from word
+//   GK_CTR_CALL to GK_CALL_BYTES):  [14] deferred streams, [15] long-stream
+//   list length, [16 + 4r + c] round r's re-run list length of class c,
+//   [40 + r] round r's overflow count, then (byte GK_CALL_WORK) the launches'
+//   stream hand-out counters.
+// The host reads words [0, GK_CTR_WORDS) back after every call.
 #define GK_CTR_USED 0
 #define GK_CTR_LCNT 4
-#define GK_CTR_RCNT 8
 #define GK_CTR_FATAL 12   // [12] count, [13] largest such stream id
 #define GK_CTR_DEFER 14   // streams whose class had no free slot this call (re-run by the host later)
+#define GK_CTR_LONG 15    // streams longer than GK_STATS_LONG values (k_stats)
+#define GK_CTR_RCNT 16    // [16 + 4*round + class]
+#define GK_CTR_OVFC 40    // [40 + round]
 #define GK_CTR_WORDS 16
+#define GK_CTR_CALL 14
+#define GK_CALL_WORK 256                          // bytes: the small-class launch's GK_WORK_BYTES, then
+#define GK_CALL_SLOTS 16                          //   16 counters of 128 bytes for the other launches
+#define GK_CALL_BYTES (GK_CALL_WORK + GK_WORK_BYTES + GK_CALL_SLOTS * 128)
 struct GKPoolDev {
   int32_t* ctr;
+  int32_t* rcnt;  // this round's re-run list lengths (one per class)
   int32_t* list[GK_MAX_CLASSES];
   int32_t* rerun[GK_MAX_CLASSES];
   int32_t* defer;  // S entries
