@@ -12,6 +12,13 @@ them).
 points depend only on the running count ``n`` (gk:60), batching the adds does
 not change any result.  One GKArray = a StreamSet of one stream: use
 ``StreamSet`` directly to sketch many streams at once.
+
+``entries`` and ``incoming`` are lists materialised from the device, and like
+the reference's attributes (gk:23-24) they may be mutated -- ``Entry`` fields,
+list items, appends -- or assigned: the next operation on the sketch writes
+the changed lists back to the device first (one ``gk_import``).  After that
+operation a list obtained before it is detached (the reference detaches
+``entries`` only at a flush, gk:108); read the attribute again.
 """
 import math
 
@@ -55,9 +62,39 @@ class GKArray:
         self._set = StreamSet(1, eps, device)
         self._buf = []
         self._offs = None
+        self._views = None  # (entries list, incoming list, snapshot) handed out, not yet written back
 
     # ---------------------------------------------------------------- plumbing
+    def _sync_views(self):
+        """Write caller mutations of ``entries`` / ``incoming`` back to the
+        device (gk:23-24 are plain attributes in the reference), then detach
+        the lists."""
+        if self._views is None:
+            return
+        ents, inc, snap = self._views
+        self._views = None
+        now = ([(e.val, e.g, e.delta) for e in ents], list(inc))
+        if now != snap:
+            self._push(now[0], now[1])
+
+    def _push(self, recs, pending):
+        """The stream's table := recs [(v, g, delta)], pending := values
+        (header words kept): one gk_import."""
+        P = self._set.flush_period
+        if len(pending) >= P:
+            raise ValueError("incoming holds %d values; at most %d fit the flush period" % (len(pending), P - 1))
+        dev = self._set.device
+        st = self._set.stats()
+        f64 = lambda a: torch.tensor(a if a else [0.0], dtype=torch.float64, device=dev)
+        i32 = lambda a: torch.tensor(a if a else [0], dtype=torch.int32, device=dev)
+        i64 = lambda a: torch.tensor(a, dtype=torch.int64, device=dev)
+        self._set.import_arrays(i64([0, len(recs)]), f64([float(r[0]) for r in recs]), i32([int(r[1]) for r in recs]),
+                                i32([int(r[2]) for r in recs]), i64([0, len(pending)]),
+                                f64([float(x) for x in pending]), st["n"].to(torch.int64), st["min"], st["max"],
+                                st["sum"], st["avg"])
+
     def _ship(self):
+        self._sync_views()
         if self._buf:
             vals = torch.tensor(self._buf, dtype=torch.float64, device=self._set.device)
             offs = torch.tensor([0, len(self._buf)], dtype=torch.int64, device=self._set.device)
@@ -107,18 +144,36 @@ class GKArray:
     def max(self):
         return self._max
 
+    def _materialise(self):
+        self._ship()
+        ents = [Entry(v, g, d) for (v, g, d) in self._set.table(0)]
+        offs, pv = self._set.pending()
+        inc = pv.cpu().tolist()
+        self._views = (ents, inc, ([(e.val, e.g, e.delta) for e in ents], list(inc)))
+        return self._views
+
     @property
     def entries(self):
-        """Materialised copy of the table (gk:23); does not flush."""
+        """The table (gk:23) as a list of Entry; does not flush.  Mutations
+        are written back by the next operation on the sketch."""
+        return self._materialise()[0]
+
+    @entries.setter
+    def entries(self, value):
         self._ship()
-        return [Entry(v, g, d) for (v, g, d) in self._set.table(0)]
+        offs, pv = self._set.pending()
+        self._push([(e.val, e.g, e.delta) for e in value], pv.cpu().tolist())
 
     @property
     def incoming(self):
-        """Pending raw values (gk:24), insertion order; does not flush."""
+        """Pending raw values (gk:24), insertion order; does not flush.
+        Mutations are written back by the next operation on the sketch."""
+        return self._materialise()[1]
+
+    @incoming.setter
+    def incoming(self, value):
         self._ship()
-        offs, pv = self._set.pending()
-        return pv.cpu().tolist()
+        self._push([(v, g, d) for (v, g, d) in self._set.table(0)], [float(x) for x in value])
 
     # ---------------------------------------------------------------- accessors
     def num_values(self):
@@ -139,6 +194,8 @@ class GKArray:
     # ---------------------------------------------------------------- ingest
     def add(self, val):
         """gk:49-61 (buffered; flush points are decided on the GPU)."""
+        if self._views is not None:
+            self._sync_views()  # caller edits of entries / incoming come first
         self._buf.append(float(val))
         if len(self._buf) >= self.SHIP_CHUNK:
             self._ship()
