@@ -186,11 +186,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # GK_BENCH_REHEARSE=1: rehearse the N-rank path on fewer GPUs (ranks share
+    # devices, gloo for the timing collectives; the numbers mean nothing)
+    rehearse = os.environ.get("GK_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local %= max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
     from gkarray_amd import StreamSet
 
     defaults = {"cfg3": (1_000_000, 1000, "pareto"), "cfg2": (100_000, 10_000, "lognormal"),
@@ -286,7 +294,7 @@ def main():
         flush_ms, stats_ms, launches = flush_ms + f_ms, stats_ms + s_ms, launches + n_l
     if world > 1:
         import torch.distributed as dist
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt], dtype=torch.float64, device="cpu" if rehearse else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
