@@ -220,6 +220,7 @@ struct GKHdrV {
   double mn, mx;
 };
 
+template <bool MINMAX = true>
 __device__ __forceinline__ void gk_hdr_issue(GKHdrV& h, const GKState& st, const int64_t* offs, int64_t s) {
   h.cls = st.cls[s];
   h.slot = st.slot[s];
@@ -228,8 +229,12 @@ __device__ __forceinline__ void gk_hdr_issue(GKHdrV& h, const GKState& st, const
   h.n = st.n[s];
   h.xo = offs[s];
   h.xe = offs[s + 1];
-  h.mn = st.mn[s];
-  h.mx = st.mx[s];
+  if constexpr (MINMAX) {
+    h.mn = st.mn[s];
+    h.mx = st.mx[s];
+  } else {
+    h.mn = h.mx = 0.0;
+  }
 }
 
 __device__ __forceinline__ int64_t rfl64(int64_t v) {
@@ -1848,13 +1853,25 @@ __device__ __forceinline__ int pidx(int i) { return i + (i >> 5); }
 // lane 0 adds the s_memtime delta since the previous mark to a per-block
 // LDS counter; the block adds its counters to gk_prof_acc when it ends.
 
+// Gaps are indexed by the PADDED slot of their entry (pidx(j), j = 0..E): the
+// gap search yields that index directly, so it addresses the counts and the
+// per-gap records without a conversion.  Padded slots 32, 65, 98 (i % 33 ==
+// 32) are never a gap.  Conditional LDS stores of the flush are branch-free:
+// a lane with nothing to store writes to a slot nobody reads (GK_SMALL_TRASH
+// in tv/tgd, the lane's own word past the counts, the last mv slot), which
+// spares the exec-mask save / restore / branch of every divergent store.
+#define GK_SMALL_TRASH (SMALL_CAP + 1)  // logical slot: tv[pidx(129)], tgd[129]
+static_assert(SMALL_CAP == 128, "k_ingest_small is laid out for the 128-entry class (K = 2 entries per lane)");
 template <int VPL>
 struct SmallLDS {
-  double tv[SMALL_TVN];         // entry values at pidx(i); +inf from E up to pow2_above(E)-2
-  int2 tgd[SMALL_CAP + 2];      // entry (g, d) at i; [j0+K] read as successor
-  uint32_t gpk[SMALL_CAP + 4];  // per gap: member count
-  int2 gi[SMALL_CAP + 2];       // per gap: (k << 16 | member base << 8 | out base, G + d - 1)
-  double mv[64 * VPL + GK_SMALL_RANK_MAX];  // pending values grouped by gap, +inf after the last
+  // first, at LDS address 0: the rank loop's reads of mv take their offsets
+  // as ds_read2_b64 immediates
+  alignas(16) double mv[64 * VPL + 64 + 2];  // values grouped by gap, +inf after the last; [last] trash
+  alignas(16) double tv[SMALL_TVN];        // entry values at pidx(i); +inf from E up to E+63 (<= 127)
+  alignas(16) int2 tgd[SMALL_CAP + 2];     // entry (g, d) at i; [j0+2] read as successor; [129] trash
+  alignas(16) uint32_t gpk[256];           // per gap (padded index): member count; [SMALL_TVN + lane] trash
+  alignas(16) int2 gi[SMALL_TVN];          // per gap (padded index): (m<<24 | k<<16 | member base<<8 | out base, G+d-1)
+  alignas(16) int32_t mi[64 * VPL + 2];    // exact rank pass: a member's insertion index; [last] trash
 #ifdef GK_LDS_PAD
   unsigned char pad[GK_LDS_PAD];  // occupancy experiments only
 #endif
@@ -1864,38 +1881,37 @@ struct SmallLDS {
 #endif
 };
 
-// gap counters of the next flush (read and written only inside a flush)
+// gap counters of the next flush (read and written only inside a flush):
+// padded indices 0 .. pidx(127) = 130
 __device__ __forceinline__ void small_zero_counts(uint32_t* gpk, int lane) {
-  if constexpr (SMALL_CAP == 128) *(uint2*)&gpk[2 * lane] = make_uint2(0u, 0u);
-  else for (int j = 4 * lane; j < SMALL_CAP; j += 256) *(uint4*)&gpk[j] = make_uint4(0u, 0u, 0u, 0u);
+  *(uint4*)&gpk[4 * lane] = make_uint4(0u, 0u, 0u, 0u);  // 0..255: the counts and the trash words
 }
 
 __device__ __forceinline__ void small_pad(double* tv, int E, int lane) {
-  if constexpr (SMALL_CAP == 128) {
-    // slots E .. pow2_above(E)-2 lie inside E .. E+63 (E <= 127); one store
-    // per lane, clamped to slot 127, which never holds an entry
-    tv[pidx(min(E + lane, SMALL_CAP - 1))] = __longlong_as_double(0x7ff0000000000000LL);
-  } else {
-    const int hi = gk_pow2_above(E) - 1;
-    for (int j = E + lane; j < hi; j += 64) tv[pidx(j)] = __longlong_as_double(0x7ff0000000000000LL);
-  }
+  // the gap search always runs its 7 levels (first probe: slot 63); slots
+  // E .. E+63 (clamped to 127, which never holds an entry) are +inf, so every
+  // probe it makes at or above E reads +inf (for E <= 63 it never passes
+  // slot 63 unless x is +inf, whose gap is clamped to E)
+  tv[pidx(min(E + lane, SMALL_CAP - 1))] = __longlong_as_double(0x7ff0000000000000LL);
 }
 
-// a / cs for 0 <= a < 256, cs = max(T,1) >= 1: cs == 1 -> a, cs >= 256 -> 0,
-// else the high half of a * ceil(2^32 / cs) (exact: a * cs < 2^16).
+// a / cs for 0 <= a < 256, cs = max(T,1) >= 1, in two full-rate VALU ops:
+// (a * m) >> 23 with m = ceil(2^23 / cs) (a 24-bit operand: v_mul_u32_u24).
+// Exact: m*cs = 2^23 + e with 0 <= e < cs, so a*m / 2^23 = a/cs + a*e/(cs 2^23)
+// and a*e < 2^16 < 2^23 keeps the floor; cs == 1: m = 2^23 gives a;
+// cs >= 256: m = 1 gives 0 = a / cs.
 struct CsDiv {
   int cs;
-  uint32_t magic;
-  int mode;  // 0: cs == 1, 1: magic, 2: cs >= 256
-  __device__ __forceinline__ int div(int a) const {
-    return mode == 0 ? a : (mode == 2 ? 0 : (int)__umulhi((uint32_t)a, magic));
-  }
+  uint32_t m;
+  __device__ __forceinline__ int div(int a) const { return (int)(__umul24((uint32_t)a, m) >> 23); }
+  // a - (a / cs) * cs (q * cs: q = 0 whenever cs >= 2^24)
+  __device__ __forceinline__ int rem(int a, int q) const { return a - (int)__umul24((uint32_t)q, (uint32_t)cs); }
 };
 
 struct CsMagicTable {
   uint32_t m[256];
   constexpr CsMagicTable() : m() {
-    for (int c = 2; c < 256; ++c) m[c] = 0xFFFFFFFFu / (uint32_t)c + 1u;
+    for (uint32_t c = 1; c < 256; ++c) m[c] = ((1u << 23) + c - 1u) / c;
   }
 };
 __constant__ CsMagicTable gk_cs_magic = CsMagicTable();
@@ -1903,8 +1919,7 @@ __constant__ CsMagicTable gk_cs_magic = CsMagicTable();
 __device__ __forceinline__ CsDiv make_csdiv(int T) {
   CsDiv c;
   c.cs = T > 1 ? T : 1;
-  c.mode = c.cs == 1 ? 0 : (c.cs >= 256 ? 2 : 1);
-  c.magic = gk_cs_magic.m[c.cs & 255];
+  c.m = c.cs < 256 ? gk_cs_magic.m[c.cs] : 1u;
   return c;
 }
 
@@ -1914,29 +1929,24 @@ __device__ __forceinline__ void small_put(SmallLDS<VPL>& L, int pos, double v, i
   L.tgd[pos] = make_int2(g, d);
 }
 
-// One value x (insertion index i) of gap `gap` at rank `rk` inside its gap:
-// gk:93-99 for gap < E, gk:85-92 for the tail.
-// gi[gap].x fields
 // gi[gap].x = m << 24 | k << 16 | member base << 8 | out base (m, k <= 128)
 __device__ __forceinline__ int gi_ob(int x) { return x & 0xff; }
 __device__ __forceinline__ int gi_mb(int x) { return (x >> 8) & 0xff; }
 __device__ __forceinline__ int gi_k(int x) { return (x >> 16) & 0xff; }
 __device__ __forceinline__ int gi_m(int x) { return (int)((uint32_t)x >> 24); }
 
-// One value x of gap `gap` (its info gi) at rank `rk` inside its gap:
-// gk:93-99 for gap < E, gk:85-92 for the tail.
+// One value x of a gap (its record gi) at rank `rk` inside the gap: gk:93-99
+// for an entry's gap, gk:85-92 for the tail.  Both rules evaluated, one store:
+// an absorbed value (or an empty slot, !valid) goes to the trash slot.
 template <int VPL>
-__device__ __forceinline__ void small_emit(SmallLDS<VPL>& L, int E, int totm, const CsDiv& cd, double x,
-                                           int gap, int2 gi, int rk) {
-  (void)totm;
-  // both rules evaluated, one store (no divergent branch per value)
-  const bool in_gap = gap < E;
+__device__ __forceinline__ void small_emit(SmallLDS<VPL>& L, bool in_gap, const CsDiv& cd, double x, int2 gi,
+                                           int rk, bool valid) {
   const int k = gi_k(gi.x);
   const int q = cd.div(rk);
-  const int rr = rk - q * cd.cs;
+  const int rr = cd.rem(rk, q);
   const int pos = gi_ob(gi.x) + (in_gap ? rk - k : q);
-  const bool keep = in_gap ? rk >= k : (rr == cd.cs - 1 || rk == gi_m(gi.x) - 1);
-  if (keep) small_put(L, pos, x, in_gap ? 1 : rr + 1, in_gap ? gi.y : 0);
+  const bool keep = valid && (in_gap ? rk >= k : (rr == cd.cs - 1 || rk == gi_m(gi.x) - 1));
+  small_put(L, keep ? pos : GK_SMALL_TRASH, x, in_gap ? 1 : rr + 1, in_gap ? gi.y : 0);
 }
 
 // ---- in-register sort of 128 doubles, two per lane ------------------------
@@ -2008,6 +2018,7 @@ __device__ __forceinline__ void sort128_2(double (&a)[2], int lane) {
 template <int VPL, int K, typename AfterSearch>
 __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const double (&xv)[VPL], const int cnt,
                                            const int T, const int lane, AfterSearch&& after_search) {
+  static_assert(K == 2, "the 128-entry class holds 2 entries per lane");
   if constexpr (VPL == 2) {
     // ---- empty table (every stream's first flush): all values are tail
     //      (gk:85-92), so the flush is a sort and a cut into chunks of
@@ -2035,8 +2046,9 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
         for (int r = 0; r < 2; ++r) {
           const int q = lane + 64 * r;  // rank in the tail
           const int c = cd.div(q);
-          const int rr = q - c * cd.cs;
-          if (q < cnt && (rr == cd.cs - 1 || q == cnt - 1)) small_put(L, c, a[r], rr + 1, 0);
+          const int rr = cd.rem(q, c);
+          const bool keep = q < cnt && (rr == cd.cs - 1 || q == cnt - 1);
+          small_put(L, keep ? c : GK_SMALL_TRASH, a[r], rr + 1, 0);
         }
         small_pad(L.tv, newE, lane);
         wsync<false>();
@@ -2045,8 +2057,11 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
       }
     }
   }
-  // ---- gap = #entries <= x (gk:93): search from the padded size down ------
-  // xb: byte offset of the padded slot of the gap's first entry
+  // ---- gap = #entries <= x (gk:93): 7 levels over the padded table ---------
+  // (slots E .. E+63 hold +inf, small_pad).  xb: byte offset of the padded
+  // slot of the gap's entry; x = +inf may step into the padding: clamped to
+  // the tail gap.  The gap's padded index addresses the counts (xb/2) and the
+  // per-gap records (xb) directly.
   int xb[VPL];
 #pragma unroll
   for (int r = 0; r < VPL; ++r) xb[r] = 0;
@@ -2059,91 +2074,65 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
     _Pragma("unroll") for (int r = 0; r < VPL; ++r) t_[r] = *(const double*)(tb + xb[r] + off_);       \
     _Pragma("unroll") for (int r = 0; r < VPL; ++r) xb[r] += (t_[r] <= xv[r]) ? step_ : 0;             \
   }
-  switch (32 - __clz(E)) {  // log2(pow2_above(E))
-    case 8: if constexpr (K > 2) GK_PROBE(128) [[fallthrough]];
-    case 7: GK_PROBE(64) [[fallthrough]];
-    case 6: GK_PROBE(32) [[fallthrough]];
-    case 5: GK_PROBE(16) [[fallthrough]];
-    case 4: GK_PROBE(8) [[fallthrough]];
-    case 3: GK_PROBE(4) [[fallthrough]];
-    case 2: GK_PROBE(2) [[fallthrough]];
-    case 1: GK_PROBE(1) [[fallthrough]];
-    default: break;
-  }
+  GK_PROBE(64)
+  GK_PROBE(32)
+  GK_PROBE(16)
+  GK_PROBE(8)
+  GK_PROBE(4)
+  GK_PROBE(2)
+  GK_PROBE(1)
 #undef GK_PROBE
-  int xg[VPL];
+  const int pE = pidx(E);           // padded index of the tail gap
+  const int pE8 = pE * (int)sizeof(double);
 #pragma unroll
-  for (int r = 0; r < VPL; ++r) {
-    const uint32_t p = (uint32_t)xb[r] >> 3;          // padded slot = b + b/32
-    xg[r] = min((int)(p - p / 33u), E);               // +inf steps into the padding
-  }
+  for (int r = 0; r < VPL; ++r) xb[r] = min(xb[r], pE8);
   after_search();
   GK_MARK(L, 1);
 
-  // ---- the lane's K entries (+ successor) into registers ------------------
+  // ---- the lane's 2 entries (+ successor) into registers ------------------
   // (the table is not written before the scan below: these reads are issued
   // beside the count atomics instead of after them)
-  const int j0 = lane * K;
+  const int j0 = 2 * lane;
+  const int pj0 = j0 + (lane >> 4);  // pidx(j0); j0 and j0+1 share a 32-slot block
   double ev[K];
   int eg[K + 1], ed[K + 1], em[K];
   {
     int2 gd[K + 1];
-    if constexpr (K == 2) {
-      const int4 a = *(const int4*)&L.tgd[j0];
-      gd[0] = make_int2(a.x, a.y);
-      gd[1] = make_int2(a.z, a.w);
-      gd[2] = L.tgd[j0 + 2];
-    } else {
-      const int4 a = *(const int4*)&L.tgd[j0];
-      const int4 b = *(const int4*)&L.tgd[j0 + 2];
-      gd[0] = make_int2(a.x, a.y);
-      gd[1] = make_int2(a.z, a.w);
-      gd[2] = make_int2(b.x, b.y);
-      gd[3] = make_int2(b.z, b.w);
-      gd[4] = L.tgd[j0 + 4];
-    }
+    const int4 a = *(const int4*)&L.tgd[j0];
+    gd[0] = make_int2(a.x, a.y);
+    gd[1] = make_int2(a.z, a.w);
+    gd[2] = L.tgd[j0 + 2];
 #pragma unroll
     for (int e = 0; e <= K; ++e) {
       const bool v = j0 + e < E;  // past E: stale LDS, masked
-      if (e < K) ev[e] = L.tv[pidx(j0 + e)];
+      if (e < K) ev[e] = L.tv[pj0 + e];
       eg[e] = v ? gd[e].x : 0;
       ed[e] = v ? gd[e].y : 0;
     }
   }
 
   // ---- gap counts and each value's slot in its gap ------------------------
-  // (the counters were zeroed at the end of the previous flush / stream setup)
+  // (the counters were zeroed at the end of the previous flush / stream
+  // setup; an empty value slot counts into its lane's trash word)
   uint32_t xs[VPL];
 #pragma unroll
-  for (int r = 0; r < VPL; ++r) xs[r] = (lane + 64 * r < cnt) ? atomicAdd(&L.gpk[xg[r]], 1u) : 0u;
+  for (int r = 0; r < VPL; ++r) {
+    uint32_t* ctr = (lane + 64 * r < cnt) ? (uint32_t*)((char*)L.gpk + (xb[r] >> 1)) : &L.gpk[SMALL_TVN + lane];
+    xs[r] = atomicAdd(ctr, 1u);
+  }
   wsync<false>();
   uint32_t mloc = 0;
 #pragma unroll
   for (int r = 0; r < VPL; ++r) mloc = max(mloc, xs[r] + 1u);
-  // +0.0 and -0.0 in one flush: only the exact (insertion-index) tie-break
-  // of the counting path orders them like the reference
-  bool pz = false, nz = false;
-#pragma unroll
-  for (int r = 0; r < VPL; ++r) {
-    const bool z = (lane + 64 * r < cnt) && xv[r] == 0.0;
-    pz |= z && !signbit(xv[r]);
-    nz |= z && signbit(xv[r]);
-  }
-  const bool use_sort = (__builtin_amdgcn_ballot_w64(mloc > (uint32_t)GK_SMALL_RANK_MAX) != 0) ||
-                        (__builtin_amdgcn_ballot_w64(pz) != 0 && __builtin_amdgcn_ballot_w64(nz) != 0);
+  // a gap of more than GK_SMALL_RANK_MAX members: rank by counting (exact,
+  // ties by insertion index, like the in-gap exact pass below)
+  const bool use_sort = __builtin_amdgcn_ballot_w64(mloc > (uint32_t)GK_SMALL_RANK_MAX) != 0;
   GK_MARK(L, 2);
 
   {
-    uint32_t mm[K];
-    if constexpr (K == 2) {
-      const uint2 v = *(const uint2*)&L.gpk[j0];
-      mm[0] = v.x; mm[1] = v.y;
-    } else {
-      const uint4 v = *(const uint4*)&L.gpk[j0];
-      mm[0] = v.x; mm[1] = v.y; mm[2] = v.z; mm[3] = v.w;
-    }
-#pragma unroll
-    for (int e = 0; e < K; ++e) em[e] = (j0 + e < E) ? (int)mm[e] : 0;
+    const uint32_t m0 = L.gpk[pj0], m1 = L.gpk[pj0 + 1];
+    em[0] = (j0 < E) ? (int)m0 : 0;
+    em[1] = (j0 + 1 < E) ? (int)m1 : 0;
   }
   int eh[K];  // g + d of the successor, -1 if none
 #pragma unroll
@@ -2201,18 +2190,18 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
     sm += (uint32_t)em[e];  // 0 past E
     so += v ? (uint32_t)(em[e] - ek[e] + (ekeep[e] ? 1 : 0)) : 0u;
   }
-  const int tail_lane = E == 0 ? 0 : (E - 1) / K;
-  int mE_tail = 0;
-  if (lane == tail_lane) {
-    const int mE = (int)L.gpk[E];
-    mE_tail = mE;
-    sm += (uint32_t)mE;
-    so += (uint32_t)(cd.cs > 128 ? (mE > 0 ? 1 : 0) : cd.div(mE + cd.cs - 1));
-  }
+  // the tail gap (uniform: one broadcast read), counted by the lane holding
+  // the last entry
+  const int tail_lane = E == 0 ? 0 : (E - 1) >> 1;
+  const int mE = __builtin_amdgcn_readfirstlane((int)L.gpk[pE]);
+  const int tail_out = cd.cs > 128 ? (mE > 0 ? 1 : 0) : cd.div(mE + cd.cs - 1);
+  sm += lane == tail_lane ? (uint32_t)mE : 0u;
+  so += lane == tail_lane ? (uint32_t)tail_out : 0u;
   const uint32_t incl = wave_incl_scan_u32((sm << 16) | so, lane);
   const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
   const int newE = (int)(total & 0xffffu);
   if (newE > SMALL_CAP - 1) return -1;  // one slot stays free for the search padding
+  const int totm = (int)(total >> 16);
   wsync<false>();                        // every lane has read the table and the counts
   GK_MARK(L, 3);
 
@@ -2222,75 +2211,77 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
     int2 gk[K];
 #pragma unroll
     for (int e = 0; e < K; ++e) {
+      const bool v = j0 + e < E;
       gk[e] = make_int2((em[e] << 24) | (ek[e] << 16) | (int)((base >> 8) & 0xff00u) | (int)(base & 0xffu),
                         eG[e] + ed[e] - 1);
-      if (j0 + e < E && ekeep[e]) small_put(L, (int)(base & 0xffffu) + em[e] - ek[e], ev[e], eG[e], ed[e]);
-      base += (j0 + e < E) ? (((uint32_t)em[e] << 16) | (uint32_t)(em[e] - ek[e] + (ekeep[e] ? 1 : 0))) : 0u;
+      small_put(L, (v && ekeep[e]) ? (int)(base & 0xffffu) + em[e] - ek[e] : GK_SMALL_TRASH, ev[e], eG[e], ed[e]);
+      base += v ? (((uint32_t)em[e] << 16) | (uint32_t)(em[e] - ek[e] + (ekeep[e] ? 1 : 0))) : 0u;
     }
-    *(int4*)&L.gi[j0] = make_int4(gk[0].x, gk[0].y, gk[1].x, gk[1].y);
-    if constexpr (K == 4) *(int4*)&L.gi[j0 + 2] = make_int4(gk[2].x, gk[2].y, gk[3].x, gk[3].y);
-    // a later store: wins over the block store of the lane owning index E
-    if (lane == tail_lane)
-      L.gi[E] = make_int2((mE_tail << 24) | (int)((base >> 8) & 0xff00u) | (int)(base & 0xffu), 0);
+    L.gi[pj0] = gk[0];
+    L.gi[pj0 + 1] = gk[1];
+    // the tail gap's record (it is last: member base totm - mE, out base
+    // newE - tail_out); a later store, so it wins over the block store of the
+    // lane owning padded index pE
+    if (lane == 0) L.gi[pE] = make_int2((mE << 24) | ((totm - mE) << 8) | (newE - tail_out), 0);
   }
-  const int totm = (int)(total >> 16);
   wsync<false>();
   GK_MARK(L, 4);
 
   // ---- stable order inside each gap (gk:72), then emit --------------------
   if (!use_sort) {
     // Members of a gap are stored in slot order (the atomic slot xs).  A
-    // value's rank in its gap counts the members below it.  Equal doubles
-    // here are bit-identical (a flush holding both +0.0 and -0.0 takes the
-    // exact path below), so the reference's insertion-order tie-break only
-    // has to give equal values distinct ranks.  Fast pass: strict counts over
-    // every member (self included: never below itself); they are the ranks
-    // iff no gap holds equal values, i.e. iff the rank sum reaches
-    // sum m(m-1)/2 -- otherwise an exact pass (ties broken by slot) reruns.
-    // The reads run past a value's own members into the next gaps (whose
-    // values are all above it: gaps partition the value range, and x < v_j
-    // <= every member of gap j+1) and, after the last member, into +inf
-    // padding: no index clamps, no member-count tests in the loop.
+    // value's rank in its gap counts the members below it.  Fast pass:
+    // strict counts over every member (self included: never below itself);
+    // they are the ranks iff no gap holds equal values, i.e. iff the rank sum
+    // reaches sum m(m-1)/2 -- otherwise an exact pass (ties broken by
+    // insertion index, Python's stable sort: also orders +0.0 / -0.0 like the
+    // reference) reruns.  The reads run past a value's own members into the
+    // next gaps (whose values are all above it: gaps partition the value
+    // range, and x < v_j <= every member of gap j+1) and, after the last
+    // member, into +inf padding: no index clamps, no member-count tests in
+    // the loop.
     int2 gv[VPL];
     int gb[VPL], mm[VPL], me[VPL];
     int omax = 0;  // this lane's largest member count; the loop runs while any lane needs it
     int dsum = 0;  // sum over this lane's values of (members - 1)
+    constexpr int MV_TRASH = 64 * VPL + 64 + 1;
 #pragma unroll
     for (int r = 0; r < VPL; ++r) {
       const bool v = lane + 64 * r < cnt;
-      gv[r] = L.gi[xg[r]];
+      gv[r] = *(const int2*)((const char*)L.gi + xb[r]);
       gb[r] = gi_mb(gv[r].x);
       const int m = v ? gi_m(gv[r].x) : 0;
       dsum += v ? m - 1 : 0;
       mm[r] = m >= 2 ? m : 0;  // a lone member has rank 0
       me[r] = (int)xs[r];
-      if (v) L.mv[gb[r] + me[r]] = xv[r];
+      L.mv[v ? gb[r] + me[r] : MV_TRASH] = xv[r];
       omax = max(omax, mm[r]);
     }
-    if (lane < GK_SMALL_RANK_MAX) L.mv[totm + lane] = __longlong_as_double(0x7ff0000000000000LL);
+    L.mv[totm + lane] = __longlong_as_double(0x7ff0000000000000LL);  // (>= GK_SMALL_RANK_MAX slots)
     wsync<false>();
     int rk[VPL];
 #pragma unroll
     for (int r = 0; r < VPL; ++r) rk[r] = 0;
-    const double* __restrict__ mvb[VPL];
-#pragma unroll
-    for (int r = 0; r < VPL; ++r) mvb[r] = L.mv + gb[r];
 #pragma unroll
     for (int u0 = 0; u0 < GK_SMALL_RANK_MAX; u0 += 2) {
       if (__builtin_amdgcn_ballot_w64(u0 < omax) == 0) break;
+      // (mv sits at LDS address 0: the reads take immediate offsets)
 #pragma unroll
       for (int r = 0; r < VPL; ++r) {
-        const double y0 = mvb[r][u0], y1 = mvb[r][u0 + 1];
-        rk[r] += (y0 < xv[r]) ? 1 : 0;
-        rk[r] += (y1 < xv[r]) ? 1 : 0;
+        const double y0 = L.mv[gb[r] + u0], y1 = L.mv[gb[r] + u0 + 1];
+        rk[r] += ((y0 < xv[r]) ? 1 : 0) + ((y1 < xv[r]) ? 1 : 0);
       }
     }
     int rsum = 0;
 #pragma unroll
-    for (int r = 0; r < VPL; ++r) rsum += rk[r];
+    for (int r = 0; r < VPL; ++r) rsum += (lane + 64 * r < cnt) ? rk[r] : 0;
     // (DPP scan: the sum wraps mod 2^32, exact for these small counts)
     if (__builtin_amdgcn_readlane((int)wave_incl_scan_u32((uint32_t)(2 * rsum - dsum), lane), 63) != 0) {
-      // equal values in some gap: exact ranks, ties broken by slot
+      // equal values in some gap: exact ranks, ties broken by insertion index
+      constexpr int MI_TRASH = 64 * VPL + 1;
+#pragma unroll
+      for (int r = 0; r < VPL; ++r) L.mi[(lane + 64 * r < cnt) ? gb[r] + me[r] : MI_TRASH] = lane + 64 * r;
+      wsync<false>();
 #pragma unroll
       for (int r = 0; r < VPL; ++r) rk[r] = 0;
       for (int u0 = 0; __builtin_amdgcn_ballot_w64(u0 < omax) != 0; u0 += 2) {
@@ -2299,15 +2290,16 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             const int u = u0 + h;
-            const double yy = L.mv[gb[r] + min(u, max(mm[r] - 1, 0))];
-            const bool below = (yy < xv[r]) | ((yy == xv[r]) & (u < me[r]));
+            const int iu = gb[r] + min(u, max(mm[r] - 1, 0));
+            const double yy = L.mv[iu];
+            const int ii = L.mi[iu];
+            const bool below = (yy < xv[r]) | ((yy == xv[r]) & (ii < lane + 64 * r));
             rk[r] += (u < mm[r] && below) ? 1 : 0;
           }
       }
     }
 #pragma unroll
-    for (int r = 0; r < VPL; ++r)
-      if (lane + 64 * r < cnt) small_emit(L, E, totm, cd, xv[r], xg[r], gv[r], rk[r]);
+    for (int r = 0; r < VPL; ++r) small_emit(L, xb[r] < pE8, cd, xv[r], gv[r], rk[r], lane + 64 * r < cnt);
     GK_MARK(L, 5);
   } else {
     // A large gap (the first flush, where every value is tail, or an
@@ -2358,10 +2350,8 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
     }
 #pragma unroll
     for (int r = 0; r < VPL; ++r) {
-      if (lane + 64 * r < cnt) {
-        const int2 gv = L.gi[xg[r]];
-        small_emit(L, E, totm, cd, xv[r], xg[r], gv, q[r] - gi_mb(gv.x));
-      }
+      const int2 gv = *(const int2*)((const char*)L.gi + xb[r]);
+      small_emit(L, xb[r] < pE8, cd, xv[r], gv, q[r] - gi_mb(gv.x), lane + 64 * r < cnt);
     }
     GK_MARK(L, 6);
   }
@@ -2599,10 +2589,13 @@ __global__ void k_qfix(GKState st, double* __restrict__ out, int nq) {
   else if (b == GK_QMARK_MAX) out[i] = st.mx[i / nq];
 }
 
-template <int VPL>
+// FS: the launch carries the stats role (nstat > 0): _min/_max are not final
+// during it, so the header prefetch skips them and fused quantiles use markers.
+// Class 0 over every stream only (promoted streams are skipped: their class's
+// launch runs them).
+template <int VPL, bool FS>
 __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st, const double* __restrict__ x,
-                                                     const int64_t* __restrict__ offs,
-                                                     const int32_t* __restrict__ list, int64_t count, int force,
+                                                     const int64_t* __restrict__ offs, int64_t count, int force,
                                                      int32_t* __restrict__ ovf_count, int32_t* __restrict__ ovf_list,
                                                      const double* __restrict__ qs, int nq,
                                                      double* __restrict__ qout, int qmode,
@@ -2629,7 +2622,7 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
 #endif
   const int nparts = (int)min((unsigned)GK_WORK_PARTS, gridDim.x);  // every part has a wave
   const int part = (int)(blockIdx.x % (unsigned)nparts);
-  if ((int)blockIdx.x < nstat) fused_stats_role(st, x, offs, work, part, nparts, count, fs_pace, fs_lag, lane);
+  if (FS && (int)blockIdx.x < nstat) fused_stats_role(st, x, offs, work, part, nparts, count, fs_pace, fs_lag, lane);
   const int64_t pbeg = count * part / nparts, pend = count * (part + 1) / nparts;
   int64_t cur = 0, cend = 0;
   auto grab = [&]() -> int64_t {
@@ -2643,9 +2636,9 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
     return cur++;
   };
   int64_t w = grab();
-  if (w < count) gk_hdr_issue(hv, st, offs, list ? (int64_t)list[w] : w);
+  if (w < count) gk_hdr_issue<!FS>(hv, st, offs, w);
   for (; w < count;) {
-    const int64_t s = list ? (int64_t)list[w] : w;
+    const int64_t s = w;
     const int64_t wn = grab();
     const int32_t scls = __builtin_amdgcn_readfirstlane(hv.cls);
     const int32_t sslot = __builtin_amdgcn_readfirstlane(hv.slot);
@@ -2655,13 +2648,11 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
     const int64_t xo = rfl64(hv.xo);
     const int64_t xe = rfl64(hv.xe);
     // with the stats role in this launch, _min/_max are not final yet: markers
-    const double smn = nstat > 0 ? __longlong_as_double(GK_QMARK_MIN)
-                                 : __longlong_as_double(rfl64(__double_as_longlong(hv.mn)));
-    const double smx = nstat > 0 ? __longlong_as_double(GK_QMARK_MAX)
-                                 : __longlong_as_double(rfl64(__double_as_longlong(hv.mx)));
-    if (wn < count) gk_hdr_issue(hv, st, offs, list ? (int64_t)list[wn] : wn);
+    const double smn = FS ? __longlong_as_double(GK_QMARK_MIN) : __longlong_as_double(rfl64(__double_as_longlong(hv.mn)));
+    const double smx = FS ? __longlong_as_double(GK_QMARK_MAX) : __longlong_as_double(rfl64(__double_as_longlong(hv.mx)));
+    if (wn < count) gk_hdr_issue<!FS>(hv, st, offs, wn);
     w = wn;
-    if (!list && scls != 0) continue;  // promoted: handled by its class launch
+    if (scls != 0) continue;  // promoted: handled by its class launch
     const int64_t Lx = xe - xo;
     // force 1: flush only if values are pending (size/quantile, gk:45, 166, 197)
     // force 2: unconditional merge_compress() (merge, gk:122, 126, 137)
@@ -3417,7 +3408,7 @@ static hipError_t launch_ingest_small(const GKState& st, const double* x, const 
   if (count <= 0) return hipSuccess;
   if (!work) return hipErrorInvalidValue;
   int occ = 0;
-  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_ingest_small<VPL>, 64, 0);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_ingest_small<VPL, false>, 64, 0);
   if (occ <= 0) occ = 1;
   // one resident wave per slot; streams are handed out through `work`
   int64_t grid = (int64_t)num_cu() * occ;
@@ -3433,8 +3424,13 @@ static hipError_t launch_ingest_small(const GKState& st, const double* x, const 
   // pacing needs ingest-only waves in every part (stats waves wait for them)
   const int pace = nstat > 0 && grid >= 4 * (int64_t)nstat && grid >= 8 * GK_WORK_PARTS ? 1 : 0;
   static const int lag = getenv("GK_FS_LAG") ? atoi(getenv("GK_FS_LAG")) : GK_FS_LAG_DEFAULT;
-  hipLaunchKernelGGL((k_ingest_small<VPL>), dim3((unsigned)grid), dim3(64), 0, stream, st, x, offs, list, count,
-                     force, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode, work, nstat, pace, lag);
+  if (list) return hipErrorInvalidValue;  // class 0 over every stream only
+  if (nstat > 0)
+    hipLaunchKernelGGL((k_ingest_small<VPL, true>), dim3((unsigned)grid), dim3(64), 0, stream, st, x, offs, count,
+                       force, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode, work, nstat, pace, lag);
+  else
+    hipLaunchKernelGGL((k_ingest_small<VPL, false>), dim3((unsigned)grid), dim3(64), 0, stream, st, x, offs, count,
+                       force, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode, work, nstat, pace, lag);
   if (nstat > 0 && q.qs && q.nq > 0) {
     const int64_t tot = st.S * (int64_t)q.nq;
     hipLaunchKernelGGL(k_qfix, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, st, q.out, q.nq);
