@@ -2687,6 +2687,11 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
     bool final_done = false;
     int64_t used = 0;
     int64_t need = P - (n % P);  // adds until n hits the next multiple of P (gk:60)
+    // float(n - 1) of gk:70, kept as a double that each flush advances by
+    // its adds (integers < 2^53: exact); T = floor((2 eps) * (n - 1)) is then
+    // a multiply and a truncation (n >= 1 at every flush, and gk_count_ok
+    // above bounds T by GK_T_CLAMP for the whole call: no clamps)
+    double nm1 = (double)(n - 1);
     double xv[VPL];
 #pragma unroll
     for (int r = 0; r < VPL; ++r) xv[r] = 0.0;
@@ -2715,7 +2720,8 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
         }
       };
       n += nadd;
-      const int T = gk_threshold(st, n);
+      nm1 += (double)(int)nadd;
+      const int T = __builtin_amdgcn_readfirstlane((int)(st.two_eps * nm1));
       GK_MARK(L, 8);
       int nE;
       if constexpr (SMALL_CAP > 128)

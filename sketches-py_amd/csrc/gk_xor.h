@@ -12,9 +12,11 @@
 #define GK_DPP_ROW_ROR8 0x128
 
 
+// full permutations (every lane has a source): no `old` operand to
+// initialise (v_mov_b32_dpp with bound_ctrl, one instruction)
 template <int CTRL>
 __device__ __forceinline__ int gk_dppmov(int v) {
-  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
+  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, true);
 }
 
 // lane ^ 16: permlane16_swap exchanges the odd rows of its first operand with
