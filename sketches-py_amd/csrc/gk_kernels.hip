@@ -21,6 +21,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <limits>
 #include <type_traits>
 
 #include "gk_state.h"
@@ -116,6 +117,17 @@ __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v, int /*lane*/)
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, DPP_ROW_SHR(8), 0xf, 0xf, false);
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, DPP_ROW_BCAST15, 0xa, 0xf, false);
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, DPP_ROW_BCAST31, 0xc, 0xf, false);
+  return v;
+}
+
+// inclusive wave64 running max of int32 (lanes without a DPP source take INT_MIN)
+__device__ __forceinline__ int32_t wave_incl_max_i32(int32_t v) {
+  v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, DPP_ROW_SHR(1), 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, DPP_ROW_SHR(2), 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, DPP_ROW_SHR(4), 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, DPP_ROW_SHR(8), 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, DPP_ROW_BCAST15, 0xa, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, DPP_ROW_BCAST31, 0xc, 0xf, false));
   return v;
 }
 
@@ -2367,73 +2379,76 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
 // running max of prefix(g) + d - 1 is monotone, so the reference's break
 // index for a threshold th is the number of entries whose running max is
 // <= th: one ballot + popcount per entry slot.
-template <int K, int VPL>
-__device__ __attribute__((noinline)) void small_quantiles(SmallLDS<VPL>& L, int E, int64_t n, double mn, double mx,
-                                                          const GKState& st, const double* __restrict__ qs, int nq,
-                                                          int qmode, double* __restrict__ out, int lane) {
-  if (n == 0 || E == 0) {
-    for (int q = lane; q < nq; q += 64) out[q] = gk_nan();
-    return;
-  }
-  if ((double)n < st.inv_eps) {  // gk:169 / gk:200
-    for (int q = lane; q < nq; q += 64) {
-      const double qv = qs[q];
-      out[q] = (qv >= 0.0 && qv <= 1.0) ? percentile_linear_at(E, qv, [&](int i) { return L.tv[pidx(i)]; })
-                                        : gk_nan();
-    }
-    return;
-  }
-  const int j0 = lane * K;
-  int64_t run[K];
+// Quantiles of one stream from the small-class table (gk:156-232): the same
+// rule as wave_quantiles, with the lane's 2 entries in registers.  The
+// running max of prefix(g) + d - 1 is monotone, so the reference's break
+// index for a threshold th is the number of entries whose running max is
+// <= th: one ballot + popcount per entry slot and quantile.  One chunk of up
+// to 64 quantiles: lane l holds q value `qv` of quantile l (qe of them, the
+// same for every stream: loaded once per wave by the caller) and gets its
+// answer back -- no memory access besides the LDS table (a callee reaches
+// global memory only through flat accesses, each a full memory wait).
+// Prefix sums in 32 bits while n < 2^31 (always, short of 2^31-value
+// streams), else 64.
+template <typename I, int VPL>
+__device__ __forceinline__ int small_rank_count(SmallLDS<VPL>& L, int E, int64_t n, double spread_d, double qv,
+                                                int qe, int lane) {
+  const int j0 = 2 * lane;
+  I run[2];
   {
-    int g[K], d[K];
-    int lsum = 0;
-#pragma unroll
-    for (int e = 0; e < K; ++e) {
-      const int2 gd = L.tgd[j0 + e];
-      g[e] = (j0 + e < E) ? gd.x : 0;
-      d[e] = gd.y;
-      lsum += g[e];  // <= n - pending of one lane's K entries
-    }
-    const int64_t bex = wave_incl_scan_i64((int64_t)lsum, lane) - (int64_t)lsum;
-    int64_t acc = bex, m = INT64_MIN;
-#pragma unroll
-    for (int e = 0; e < K; ++e) {
-      acc += g[e];
-      const int64_t a = acc + d[e] - 1;
-      if (j0 + e < E && a > m) m = a;
-      run[e] = m;
-    }
-    const int64_t pm = wave_incl_max_i64(m, lane);
-    const int64_t pex = wave_shr1_i64(pm, INT64_MIN);
-#pragma unroll
-    for (int e = 0; e < K; ++e) run[e] = (j0 + e < E) ? (run[e] > pex ? run[e] : pex) : INT64_MAX;
+    const int4 gd = *(const int4*)&L.tgd[j0];
+    const int g0 = (j0 < E) ? gd.x : 0, g1 = (j0 + 1 < E) ? gd.z : 0;
+    const I lsum = (I)g0 + (I)g1;
+    I bex;
+    if constexpr (sizeof(I) == 4) bex = (I)wave_incl_scan_u32((uint32_t)lsum, lane) - lsum;
+    else bex = wave_incl_scan_i64(lsum, lane) - lsum;
+    const I a0 = bex + g0 + gd.y - 1, a1 = bex + g0 + g1 + gd.w - 1;
+    const I lo = std::numeric_limits<I>::min();
+    I m = (j0 < E) ? a0 : lo;
+    run[0] = m;
+    if (j0 + 1 < E && a1 > m) m = a1;
+    run[1] = m;
+    I pm;
+    if constexpr (sizeof(I) == 4) pm = (I)wave_incl_max_i32((int32_t)m);
+    else pm = wave_incl_max_i64(m, lane);
+    I pex;
+    if constexpr (sizeof(I) == 4) pex = (I)wave_shr1((int)pm, (int)lo);
+    else pex = wave_shr1_i64(pm, lo);
+    const I hi = std::numeric_limits<I>::max();
+    run[0] = (j0 < E) ? (run[0] > pex ? run[0] : pex) : hi;
+    run[1] = (j0 + 1 < E) ? (run[1] > pex ? run[1] : pex) : hi;
   }
-  const int64_t spread = (int64_t)(st.eps * (double)(n - 1));  // gk:174 / gk:210
-  for (int q0 = 0; q0 < nq; q0 += 64) {
-    int myi = 0;
-    const int qe = min(nq - q0, 64);
-    for (int qq = 0; qq < qe; ++qq) {
-      const double qv = qs[q0 + qq];
-      const bool valid = (qv >= 0.0 && qv <= 1.0);
-      const int64_t rank = valid ? (int64_t)(qv * (double)(n - 1) + 1.0) : 0;  // gk:173
-      const int64_t th = rank + spread;
-      int c = 0;
-#pragma unroll
-      for (int e = 0; e < K; ++e) c += __popcll(__builtin_amdgcn_ballot_w64(run[e] <= th));
-      if (lane == qq) myi = c;
-    }
-    if (lane < qe) {
-      const double qv = qs[q0 + lane];
-      const bool valid = (qv >= 0.0 && qv <= 1.0);
-      double r;
-      if (!valid) r = gk_nan();
-      else if (myi == 0) r = mn;                                  // gk:182-183 / gk:220
-      else if (myi < E) r = L.tv[pidx(myi - 1)];                  // gk:185 / gk:220
-      else r = (qmode == 0) ? mx : L.tv[pidx(E - 1)];             // gk:229 / gk:185
-      out[q0 + lane] = r;
-    }
+  const double nm1 = (double)(n - 1);
+  int myi = 0;
+  for (int qq = 0; qq < qe; ++qq) {
+    const double q = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(qv), qq),
+                                      __builtin_amdgcn_readlane(__double2loint(qv), qq));
+    const bool valid = (q >= 0.0 && q <= 1.0);
+    // rank = int(q*(n-1) + 1) (gk:173), threshold rank + spread (gk:174-178)
+    const int64_t th = valid ? (int64_t)(q * nm1 + 1.0) + (int64_t)spread_d : 0;
+    const I t = (I)th;
+    const int c = __popcll(__builtin_amdgcn_ballot_w64(run[0] <= t)) + __popcll(__builtin_amdgcn_ballot_w64(run[1] <= t));
+    if (lane == qq) myi = c;
   }
+  return myi;
+}
+
+template <int VPL>
+__device__ __attribute__((noinline)) double small_quantiles(SmallLDS<VPL>& L, int E, int64_t n, double mn, double mx,
+                                                            double inv_eps, double eps, double qv, int qe, int qmode,
+                                                            int lane) {
+  const bool valid = (qv >= 0.0 && qv <= 1.0);
+  if (n == 0 || E == 0) return gk_nan();
+  if ((double)n < inv_eps)  // gk:169 / gk:200
+    return valid ? percentile_linear_at(E, qv, [&](int i) { return L.tv[pidx(i)]; }) : gk_nan();
+  const double spread_d = floor(eps * (double)(n - 1));  // int(eps*(n-1)) (gk:174 / gk:210), >= 0
+  // prefix(g) + d <= n + T < 2^31 - 1 in 32 bits
+  const int myi = n < ((int64_t)1 << 30) ? small_rank_count<int32_t>(L, E, n, spread_d, qv, qe, lane)
+                                         : small_rank_count<int64_t>(L, E, n, spread_d, qv, qe, lane);
+  if (!valid) return gk_nan();
+  if (myi == 0) return mn;                          // gk:182-183 / gk:220
+  if (myi < E) return L.tv[pidx(myi - 1)];          // gk:185 / gk:220
+  return (qmode == 0) ? mx : L.tv[pidx(E - 1)];     // gk:229 / gk:185
 }
 
 // ---- stats role of the small-class launch (gk:52-59) ----------------------
@@ -2624,6 +2639,8 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
   const int part = (int)(blockIdx.x % (unsigned)nparts);
   if (FS && (int)blockIdx.x < nstat) fused_stats_role(st, x, offs, work, part, nparts, count, fs_pace, fs_lag, lane);
   const int64_t pbeg = count * part / nparts, pend = count * (part + 1) / nparts;
+  // the query's q values, the same for every stream: lane l holds q l
+  const double qpre = (qs && lane < nq) ? qs[lane] : 0.0;
   int64_t cur = 0, cend = 0;
   auto grab = [&]() -> int64_t {
     if (cur >= cend) {
@@ -2768,17 +2785,24 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
       continue;
     }
     if (qs) {
-      if constexpr (SMALL_CAP > 128) {
-        if (E <= 127) small_quantiles<2>(L, E, n, smn, smx, st, qs, nq, qmode, qout + s * (int64_t)nq, lane);
-        else small_quantiles<4>(L, E, n, smn, smx, st, qs, nq, qmode, qout + s * (int64_t)nq, lane);
-      } else {
-        small_quantiles<2>(L, E, n, smn, smx, st, qs, nq, qmode, qout + s * (int64_t)nq, lane);
+      for (int q0 = 0; q0 < nq; q0 += 64) {
+        const double qv = nq <= 64 ? qpre : ((q0 + lane < nq) ? qs[q0 + lane] : 0.0);
+        const double r = small_quantiles<VPL>(L, E, n, smn, smx, st.inv_eps, st.eps, qv, min(nq - q0, 64), qmode, lane);
+        if (q0 + lane < nq) qout[s * (int64_t)nq + q0 + lane] = r;
       }
     }
-    for (int j = lane; j < E; j += 64) {
-      const double v = L.tv[pidx(j)];
-      const int2 gd = L.tgd[j];
-      ((int4*)tab)[j] = make_int4(__double2loint(v), __double2hiint(v), gd.x, gd.y);
+    {
+      // E <= 127: two records per lane, all LDS reads before the 16-byte stores
+      double v[2];
+      int2 gd[2];
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        v[r] = L.tv[pidx(lane + 64 * r)];
+        gd[r] = L.tgd[lane + 64 * r];
+      }
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+        if (lane + 64 * r < E) ((int4*)tab)[lane + 64 * r] = make_int4(__double2loint(v[r]), __double2hiint(v[r]), gd[r].x, gd[r].y);
     }
     if (lane == 0) {
       st.n[s] = n;
