@@ -2135,12 +2135,12 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
   // ---- gap counts and each value's slot in its gap ------------------------
   // (the counters were zeroed at the end of the previous flush / stream
   // setup; an empty value slot counts into its lane's trash word)
+  // (exec-masked, not redirected: an idle lane's trash word would share the
+  // LDS banks of the live counters and add conflicts)
   uint32_t xs[VPL];
 #pragma unroll
-  for (int r = 0; r < VPL; ++r) {
-    uint32_t* ctr = (lane + 64 * r < cnt) ? (uint32_t*)((char*)L.gpk + (xb[r] >> 1)) : &L.gpk[SMALL_TVN + lane];
-    xs[r] = atomicAdd(ctr, 1u);
-  }
+  for (int r = 0; r < VPL; ++r)
+    xs[r] = (lane + 64 * r < cnt) ? atomicAdd((uint32_t*)((char*)L.gpk + (xb[r] >> 1)), 1u) : 0u;
   wsync<false>();
   uint32_t mloc = 0;
 #pragma unroll
