@@ -60,6 +60,9 @@ int vpl_for(int P) {
 }  // namespace
 
 struct gk_set {
+  // no stream is in a class above 0 (creation, gk_reset; cleared by every
+  // enqueued promotion): the member-list launches of run_ingest are skipped
+  bool no_members = true;
   int64_t S = 0;
   double eps = 0;
   int P = 0;
@@ -470,6 +473,7 @@ int promote_rounds(gk_set* h, const double* x, const int64_t* offs, int force, c
   for (int r = 1; r <= R; ++r) {
     int32_t* rcnt = h->d_ctr + GK_CTR_RCNT + GK_MAX_CLASSES * r;  // zeroed at the start of the call
     pool.rcnt = rcnt;
+    h->no_members = false;
     HIP_TRY(gk_launch_promote_dev(h->st, ovf_count(h, r - 1), ovf_list(h, r - 1), -1, pool, stream));
     if (g_trace) {
       HIP_TRY(hipStreamSynchronize(stream));
@@ -505,8 +509,9 @@ int run_ingest(gk_set* h, const double* x, const int64_t* offs, int force, hipSt
   HIP_TRY(launch_class(h, 0, x, offs, nullptr, nullptr, 0, force, q, stream, prio && x != nullptr));
   hipEvent_t t1 = timed ? timing_event(h->tev_flush, h->n_flush) : nullptr;
   if (t1) HIP_TRY(hipEventRecord(t1, stream));
-  for (int c = 1; c < R; ++c)
-    HIP_TRY(launch_class(h, c, x, offs, h->d_list[c], h->d_ctr + GK_CTR_LCNT + c, 0, force, q, stream));
+  if (!h->no_members)
+    for (int c = 1; c < R; ++c)
+      HIP_TRY(launch_class(h, c, x, offs, h->d_list[c], h->d_ctr + GK_CTR_LCNT + c, 0, force, q, stream));
   return promote_rounds(h, x, offs, force, q, stream);
 }
 
@@ -525,6 +530,7 @@ int run_merge(gk_set* dst, const MergeArgsHost& base, hipStream_t s) {
       // streams below this class move up so that their output may grow
       int rc = grow_class(dst, level, (int64_t)dst->st.alloc[level] + todo, s);
       if (rc) return rc;
+      dst->no_members = false;
       HIP_TRY(gk_launch_promote_dev(dst->st, ovf_count(dst, level - 1), ovf_list(dst, level - 1), level, pool, s));
     }
     a.dst = dst->st;
@@ -755,6 +761,7 @@ int gk_reset(gk_set* h, void* stream) {
   // a readback still in flight carries it)
   HIP_TRY(hipMemsetAsync(h->d_ctr, 0, GK_CTR_FATAL * sizeof(int32_t), s));
   HIP_TRY(gk_launch_reset(h->st, s));
+  h->no_members = true;
   return GK_OK;
 }
 
@@ -1020,6 +1027,7 @@ int gk_import(gk_set* h, const int64_t* offs, const double* v, const int32_t* g,
     if (c == 0) return GK_OK;
     rc = grow_targets(h, ovf_list(h, 0), c, s);
     if (rc) return rc;
+    h->no_members = false;
     HIP_TRY(gk_launch_promote_dev(h->st, ovf_count(h, 0), ovf_list(h, 0), -2, pool, s));
     rc = mark_done(h, s);
     if (!rc) rc = gk_sync(h, stream);

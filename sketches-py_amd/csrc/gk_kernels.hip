@@ -378,6 +378,17 @@ __global__ __launch_bounds__(256) void k_stats(GKState st, const double* __restr
   }
 }
 
+// k_stats with lengths_only, without the chains' LDS tile (whose 35 KiB per
+// block hold k_stats to 4 blocks per CU): one stream per thread, the pre-call
+// n snapshot and the long-stream list.  28 -> ~6 us per 10^6 streams.
+__global__ __launch_bounds__(256) void k_lengths(GKState st, const int64_t* __restrict__ offs,
+                                                 int32_t* __restrict__ long_list, int32_t* __restrict__ long_count) {
+  const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (s >= st.S) return;
+  st.n0[s] = st.n[s];
+  if (offs[s + 1] - offs[s] > GK_STATS_LONG) long_list[atomicAdd(long_count, 1)] = (int32_t)s;
+}
+
 // ===========================================================================
 // k_long_prep: the long-stream list k_stats built (in atomic order) sorted by
 // length, longest first (ties: lower stream id first), so that k_ingest and
@@ -671,6 +682,7 @@ __global__ __launch_bounds__(64) void k_stats_long(GKState st, const double* __r
                                                    const int64_t* __restrict__ list_n,
                                                    const int32_t* __restrict__ count) {
   __shared__ double2 buf[64];
+  __shared__ double rtile[64];
   const int lane = threadIdx.x;
   const int cnt = *count;
   if (cnt <= GK_SL_BCAST) {
@@ -717,15 +729,34 @@ __global__ __launch_bounds__(64) void k_stats_long(GKState st, const double* __r
 #pragma unroll
       for (int j = 0; j < 8; ++j) ring[d][j] = src[j];
     }
+    // Uniform group: every active lane starts at the same n with the same
+    // number of full chunks (cfg4: equal-length rows).  Then the gk:54
+    // factors 1.0/n are the same for all lanes: the wave computes 64 of them
+    // at once (lane j: 1.0/(n+1+j), one IEEE division per 64 values) into
+    // LDS every 4 chunks, and a chunk reads its 16 as broadcast LDS loads --
+    // instead of 16 divisions per lane and chunk (~15 of a step's ~27 VALU).
+    const uint64_t am = __builtin_amdgcn_ballot_w64(act);
+    const int fl = am ? __builtin_amdgcn_readfirstlane(__builtin_ffsll((long long)am) - 1) : 0;
+    const int64_t n_f = __shfl(n, fl, 64), nch_f = __shfl(nch, fl, 64);
+    const bool uni = __builtin_amdgcn_ballot_w64(act && (n != n_f || nch != nch_f)) == 0;
     for (int64_t c0 = 0; c0 < maxch; c0 += SL_DEPTH) {
 #pragma unroll
       for (int d = 0; d < SL_DEPTH; ++d) {
         const int64_t c = c0 + d;
+        if (uni && c < nch_f && (c & 3) == 0) {
+          rtile[lane] = 1.0 / (double)(n_f + 16 * c + 1 + lane);
+          wsync<false>();
+        }
         if (c < nch) {
           // reciprocals 1.0/n off the chain (IEEE divisions), then the chain
           double rc[16];
+          if (uni) {
 #pragma unroll
-          for (int k = 0; k < 16; ++k) rc[k] = 1.0 / (double)(n + 1 + k);
+            for (int k = 0; k < 16; ++k) rc[k] = rtile[16 * (int)(c & 3) + k];
+          } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) rc[k] = 1.0 / (double)(n + 1 + k);
+          }
 #pragma unroll
           for (int k = 0; k < 16; ++k) {
             const double v = (k & 1) ? ring[d][k >> 1].y : ring[d][k >> 1].x;
@@ -736,6 +767,7 @@ __global__ __launch_bounds__(64) void k_stats_long(GKState st, const double* __r
           }
           n += 16;                          // gk:52
         }
+        if (uni && (c & 3) == 3) wsync<false>();  // rtile is rewritten at the next chunk
         // refill this slot with the chunk SL_DEPTH ahead (unconditional load)
         const int64_t nx = c + SL_DEPTH;
         const double2* src = (nx < nch) ? p2 + nx * 8 : dummy;
@@ -3531,8 +3563,10 @@ hipError_t gk_launch_stats(const GKState& st, const double* x, const int64_t* of
                            hipStream_t stream) {
   if (st.S <= 0) return hipSuccess;
   const int64_t grid = (st.S + 255) / 256;
-  hipLaunchKernelGGL(k_stats, dim3((unsigned)grid), dim3(256), 0, stream, st, x, offs, long_list, long_count,
-                     lengths_only);
+  if (lengths_only)
+    hipLaunchKernelGGL(k_lengths, dim3((unsigned)grid), dim3(256), 0, stream, st, offs, long_list, long_count);
+  else
+    hipLaunchKernelGGL(k_stats, dim3((unsigned)grid), dim3(256), 0, stream, st, x, offs, long_list, long_count, 0);
   hipLaunchKernelGGL(k_long_prep, dim3(1), dim3(1024), 0, stream, st, offs, long_list, long_n,
                      (const int32_t*)long_count, ps.list_ws, ps.list_b0, ps.ws_cap, ps.ws_need);
   return hipGetLastError();

@@ -406,6 +406,27 @@ def test_many_long_streams_grouped_stats(gpu_device):
         assert_same_state(ss, osx, "grouped long state part %d" % part)
 
 
+def test_many_long_streams_uniform_n_stats(gpu_device):
+    """Equal-length long streams (cfg4's rows): every lane of a k_stats_long
+    group starts at the same n, so the gk:54 factors 1.0/n come from a
+    64-entry LDS tile per 4 chunks instead of per-lane divisions.  1100
+    streams (the last group 12 lanes), three calls (n carried), then a call
+    whose lengths differ per stream (the per-lane path after the tile path)."""
+    rng = np.random.default_rng(59)
+    S = 1100
+    ss = _ss(S, 0.01, gpu_device)
+    osx = OracleSet(S, 0.01)
+    for part, L in enumerate([16400, 16448, 20000, None]):
+        lens = [L] * S if L else list(rng.integers(16385, 17000, S))
+        seqs = [gen(int(d), int(n), rng) for d, n in zip(rng.integers(0, 8, S), lens)]
+        flat, offs = csr(seqs)
+        got = ss.ingest(torch.from_numpy(flat), torch.from_numpy(offs), quantiles=[0.5, 1.0])
+        osx.ingest(flat, offs)
+        assert_same_quantiles(got.cpu().numpy(), osx.quantiles([0.5, 1.0]), "uniform long q part %d" % part,
+                              small_of(osx, 0.01))
+        assert_same_state(ss, osx, "uniform long state part %d" % part)
+
+
 @pytest.mark.parametrize("eps", [0.05, 0.01, 0.001])
 def test_merge_compress_records_vs_oracle(gpu_device, eps):
     """merge_compress(entries) with explicit (v, g, delta) records (gk:63-109):
