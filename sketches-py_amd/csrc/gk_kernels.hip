@@ -2805,6 +2805,7 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
       flushed = true;
 #pragma unroll
       for (int r = 0; r < VPL; ++r) xv[r] = (lane + 64 * r < navail) ? xn[r] : 0.0;
+      GK_MARK(L, 10);  // (profiling builds: the wait for the prefetched values)
       if (!autof) {
         final_done = true;
         break;

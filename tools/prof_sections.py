@@ -22,7 +22,8 @@ import torch  # noqa: E402
 
 SECTIONS = ["stream setup (header, table load)", "gap search", "counts (zero, atomics, max gap)",
             "entries + carry + scan", "keeps + per-gap info", "rank loop + emit", "bitonic sort + emit",
-            "pad + end of flush", "between flushes (values, T)", "leftover, quantiles, write-back", "-", "-"]
+            "pad + end of flush", "between flushes (T, next flush setup)", "leftover, quantiles, write-back",
+            "next flush's values (prefetch wait)", "-"]
 
 SECTIONS_BIG = ["stream setup (header, table load)", "gap search", "counts (zero, atomics, max gap)",
                 "carry walk (rounds)", "sums + scan + keeps", "rank loop + emit", "bitonic sort + emit",
