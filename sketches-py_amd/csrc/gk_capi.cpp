@@ -438,15 +438,18 @@ bool stats_fused(const gk_set* h) { return h->fused_stats > 0 && h->st.cap[0] ==
 int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s) {
   hipEvent_t t0 = h->timing ? timing_event(h->tev_stats, h->n_stats) : nullptr;
   if (t0) HIP_TRY(hipEventRecord(t0, s));
-  // k_stats + k_long_prep, then the fork (k_stats_long needs only the
-  // sorted list and the pre-call n), then the presort of the long streams'
-  // flush batches on `s`
+  // the long-stream list (k_lengths) + k_long_prep, then the fork
+  // (k_stats_long needs only the sorted list and the pre-call n: the longest
+  // chains start at once), then on `s` the short streams' chains (k_stats,
+  // unless the small-class launch walks them) and the presort of the long
+  // streams' flush batches
   HIP_TRY(gk_launch_stats(h->st, x, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->ps,
                           stats_fused(h) ? 1 : 0, s));
   HIP_TRY(hipEventRecord(h->ev_fork, s));
   HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_fork, 0));
   HIP_TRY(gk_launch_stats_long(h->st, x, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->aux));
   HIP_TRY(hipEventRecord(h->ev_join, h->aux));
+  if (!stats_fused(h)) HIP_TRY(gk_launch_stats_short(h->st, x, offs, s));
   HIP_TRY(gk_launch_presort(h->st, x, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->ps, s));
   if (h->ps.ws_need) HIP_TRY(hipMemcpyAsync(h->h_ws_need, h->ps.ws_need, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   hipEvent_t t1 = h->timing ? timing_event(h->tev_stats, h->n_stats) : nullptr;

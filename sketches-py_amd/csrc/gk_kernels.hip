@@ -279,6 +279,8 @@ __global__ __launch_bounds__(256) void k_stats(GKState st, const double* __restr
                                                const int64_t* __restrict__ offs,
                                                int32_t* __restrict__ long_list, int32_t* __restrict__ long_count,
                                                int lengths_only) {
+  // long_list == nullptr: k_lengths listed the long streams already (they
+  // are skipped here, not listed again)
   __shared__ double tile[256 * STATS_ROW];
   __shared__ int64_t so[257];
   __shared__ int64_t smax;
@@ -299,7 +301,7 @@ __global__ __launch_bounds__(256) void k_stats(GKState st, const double* __restr
     st.n0[s0 + t] = st.n[s0 + t];
   }
   if (L > GK_STATS_LONG) {  // walked by k_stats_long, not in this block's trip count
-    long_list[atomicAdd(long_count, 1)] = (int32_t)(s0 + t);
+    if (long_list) long_list[atomicAdd(long_count, 1)] = (int32_t)(s0 + t);
     L = 0;
   }
   // block-uniform trip count: the longest stream of the block
@@ -3564,12 +3566,23 @@ hipError_t gk_launch_stats(const GKState& st, const double* x, const int64_t* of
                            hipStream_t stream) {
   if (st.S <= 0) return hipSuccess;
   const int64_t grid = (st.S + 255) / 256;
-  if (lengths_only)
-    hipLaunchKernelGGL(k_lengths, dim3((unsigned)grid), dim3(256), 0, stream, st, offs, long_list, long_count);
-  else
-    hipLaunchKernelGGL(k_stats, dim3((unsigned)grid), dim3(256), 0, stream, st, x, offs, long_list, long_count, 0);
+  // the long-stream list first (k_lengths, a few us), so that the caller can
+  // fork k_stats_long -- the sequential chains of the longest streams, the
+  // critical path of a Zipf batch -- before the short streams' chains
+  // (gk_launch_stats_short) run on this stream
+  (void)x;
+  (void)lengths_only;
+  hipLaunchKernelGGL(k_lengths, dim3((unsigned)grid), dim3(256), 0, stream, st, offs, long_list, long_count);
   hipLaunchKernelGGL(k_long_prep, dim3(1), dim3(1024), 0, stream, st, offs, long_list, long_n,
                      (const int32_t*)long_count, ps.list_ws, ps.list_b0, ps.ws_cap, ps.ws_need);
+  return hipGetLastError();
+}
+
+hipError_t gk_launch_stats_short(const GKState& st, const double* x, const int64_t* offs, hipStream_t stream) {
+  if (st.S <= 0) return hipSuccess;
+  const int64_t grid = (st.S + 255) / 256;
+  hipLaunchKernelGGL(k_stats, dim3((unsigned)grid), dim3(256), 0, stream, st, x, offs, (int32_t*)nullptr,
+                     (int32_t*)nullptr, 0);
   return hipGetLastError();
 }
 

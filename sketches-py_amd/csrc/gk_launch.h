@@ -88,6 +88,9 @@ struct GKPresort {
 hipError_t gk_launch_stats(const GKState& st, const double* x, const int64_t* offs, int32_t* long_list,
                            int64_t* long_n, int32_t* long_count, const GKPresort& ps, int lengths_only,
                            hipStream_t stream);
+// gk:52-59 chains of the streams up to GK_STATS_LONG values (k_stats; the
+// long ones are k_stats_long's), when class 0 is not the small class
+hipError_t gk_launch_stats_short(const GKState& st, const double* x, const int64_t* offs, hipStream_t stream);
 // k_presort over the plan k_long_prep wrote (no-op without a workspace)
 hipError_t gk_launch_presort(const GKState& st, const double* x, const int64_t* offs, const int32_t* long_list,
                              const int64_t* long_n, const int32_t* long_count, const GKPresort& ps,
