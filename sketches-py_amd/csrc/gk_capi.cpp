@@ -443,8 +443,7 @@ int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s) {
   // chains start at once), then on `s` the short streams' chains (k_stats,
   // unless the small-class launch walks them) and the presort of the long
   // streams' flush batches
-  HIP_TRY(gk_launch_stats(h->st, x, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->ps,
-                          stats_fused(h) ? 1 : 0, s));
+  HIP_TRY(gk_launch_stats(h->st, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->ps, s));
   HIP_TRY(hipEventRecord(h->ev_fork, s));
   HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_fork, 0));
   HIP_TRY(gk_launch_stats_long(h->st, x, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->aux));

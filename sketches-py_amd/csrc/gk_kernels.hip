@@ -260,7 +260,8 @@ __device__ __forceinline__ GKRec* gk_table_ptr_cs(const GKState& st, int64_t s, 
 }
 
 // ===========================================================================
-// k_stats: gk:52-59 for every value.  The _sum/_avg updates are a dependent
+// k_stats: gk:52-59 for every value of the streams up to GK_STATS_LONG values
+// (when the small-class launch does not walk them itself).  The _sum/_avg updates are a dependent
 // float64 chain in insertion order, so each stream's chain runs on one lane
 // (a 256-thread block = 256 streams).  The block stages its streams' values
 // through LDS in chunks of STATS_CHUNK values per stream: 16 lanes load one
@@ -276,11 +277,9 @@ __device__ __forceinline__ GKRec* gk_table_ptr_cs(const GKState& st, int64_t s, 
 #define STATS_ROW (STATS_CHUNK + 1)  // +1 double: lanes' rows start on different banks
 
 __global__ __launch_bounds__(256) void k_stats(GKState st, const double* __restrict__ x,
-                                               const int64_t* __restrict__ offs,
-                                               int32_t* __restrict__ long_list, int32_t* __restrict__ long_count,
-                                               int lengths_only) {
-  // long_list == nullptr: k_lengths listed the long streams already (they
-  // are skipped here, not listed again)
+                                               const int64_t* __restrict__ offs) {
+  // (the long streams were listed by k_lengths and are k_stats_long's: they
+  // are skipped here)
   __shared__ double tile[256 * STATS_ROW];
   __shared__ int64_t so[257];
   __shared__ int64_t smax;
@@ -294,22 +293,14 @@ __global__ __launch_bounds__(256) void k_stats(GKState st, const double* __restr
   }
   __syncthreads();
   int64_t L = 0;
-  if (t < nstr) {
-    L = so[t + 1] - so[t];
-    // pre-call n for the stats role of the small-class launch that follows
-    // (its ingest waves rewrite st.n[s] while the role still walks stream s)
-    st.n0[s0 + t] = st.n[s0 + t];
-  }
-  if (L > GK_STATS_LONG) {  // walked by k_stats_long, not in this block's trip count
-    if (long_list) long_list[atomicAdd(long_count, 1)] = (int32_t)(s0 + t);
-    L = 0;
-  }
+  if (t < nstr) L = so[t + 1] - so[t];
+  if (L > GK_STATS_LONG) L = 0;  // walked by k_stats_long, not in this block's trip count
   // block-uniform trip count: the longest stream of the block
   atomicMax((unsigned long long*)&smax, (unsigned long long)L);
   __syncthreads();
   const int64_t maxL = smax;
   // lengths only: the long list; the chains run in the small-class launch
-  if (maxL == 0 || lengths_only) return;
+  if (maxL == 0) return;
   const int64_t s = s0 + t;
   int64_t n = 0;
   double mn = 0, mx = 0, sm = 0, av = 0;
@@ -380,9 +371,11 @@ __global__ __launch_bounds__(256) void k_stats(GKState st, const double* __restr
   }
 }
 
-// k_stats with lengths_only, without the chains' LDS tile (whose 35 KiB per
-// block hold k_stats to 4 blocks per CU): one stream per thread, the pre-call
-// n snapshot and the long-stream list.  28 -> ~6 us per 10^6 streams.
+// The long-stream list (streams past GK_STATS_LONG values, for k_long_prep /
+// k_stats_long) and the pre-call n snapshot st.n0 (read by the small-class
+// launch's stats role while its ingest waves rewrite st.n): one stream per
+// thread, no LDS (~6 us per 10^6 streams; as part of k_stats, whose 35 KiB
+// chain tile holds it to 4 blocks per CU, it took 28 us).
 __global__ __launch_bounds__(256) void k_lengths(GKState st, const int64_t* __restrict__ offs,
                                                  int32_t* __restrict__ long_list, int32_t* __restrict__ long_count) {
   const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -3561,17 +3554,14 @@ hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x
   }
 }
 
-hipError_t gk_launch_stats(const GKState& st, const double* x, const int64_t* offs, int32_t* long_list,
-                           int64_t* long_n, int32_t* long_count, const GKPresort& ps, int lengths_only,
-                           hipStream_t stream) {
+hipError_t gk_launch_stats(const GKState& st, const int64_t* offs, int32_t* long_list, int64_t* long_n,
+                           int32_t* long_count, const GKPresort& ps, hipStream_t stream) {
   if (st.S <= 0) return hipSuccess;
   const int64_t grid = (st.S + 255) / 256;
   // the long-stream list first (k_lengths, a few us), so that the caller can
   // fork k_stats_long -- the sequential chains of the longest streams, the
   // critical path of a Zipf batch -- before the short streams' chains
   // (gk_launch_stats_short) run on this stream
-  (void)x;
-  (void)lengths_only;
   hipLaunchKernelGGL(k_lengths, dim3((unsigned)grid), dim3(256), 0, stream, st, offs, long_list, long_count);
   hipLaunchKernelGGL(k_long_prep, dim3(1), dim3(1024), 0, stream, st, offs, long_list, long_n,
                      (const int32_t*)long_count, ps.list_ws, ps.list_b0, ps.ws_cap, ps.ws_need);
@@ -3581,8 +3571,7 @@ hipError_t gk_launch_stats(const GKState& st, const double* x, const int64_t* of
 hipError_t gk_launch_stats_short(const GKState& st, const double* x, const int64_t* offs, hipStream_t stream) {
   if (st.S <= 0) return hipSuccess;
   const int64_t grid = (st.S + 255) / 256;
-  hipLaunchKernelGGL(k_stats, dim3((unsigned)grid), dim3(256), 0, stream, st, x, offs, (int32_t*)nullptr,
-                     (int32_t*)nullptr, 0);
+  hipLaunchKernelGGL(k_stats, dim3((unsigned)grid), dim3(256), 0, stream, st, x, offs);
   return hipGetLastError();
 }
 

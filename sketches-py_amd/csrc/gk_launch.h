@@ -85,9 +85,9 @@ struct GKPresort {
   int64_t ws_cap = 0;
   int64_t* ws_need = nullptr;  // device, 1 value
 };
-hipError_t gk_launch_stats(const GKState& st, const double* x, const int64_t* offs, int32_t* long_list,
-                           int64_t* long_n, int32_t* long_count, const GKPresort& ps, int lengths_only,
-                           hipStream_t stream);
+// the long-stream list + pre-call n (k_lengths), then k_long_prep
+hipError_t gk_launch_stats(const GKState& st, const int64_t* offs, int32_t* long_list, int64_t* long_n,
+                           int32_t* long_count, const GKPresort& ps, hipStream_t stream);
 // gk:52-59 chains of the streams up to GK_STATS_LONG values (k_stats; the
 // long ones are k_stats_long's), when class 0 is not the small class
 hipError_t gk_launch_stats_short(const GKState& st, const double* x, const int64_t* offs, hipStream_t stream);
