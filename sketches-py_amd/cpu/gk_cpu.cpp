@@ -645,8 +645,8 @@ int gk_import(gk_set* h, const int64_t* offs, const double* v, const int32_t* g,
   if (rc) return rc;
   if (!offs || !poffs || !n || !mn || !mx || !sum || !avg) return fail(GK_E_ARG, "null pointer");
   for (int64_t s = 0; s < h->S; ++s)
-    if (offs[s + 1] < offs[s] || poffs[s + 1] < poffs[s] || poffs[s + 1] - poffs[s] >= h->P)
-      return fail(GK_E_ARG, "stream %lld: bad table / pending sizes", (long long)s);
+    if (offs[s + 1] < offs[s] || poffs[s + 1] < poffs[s] || n[s] < 0 || poffs[s + 1] - poffs[s] > n[s] % h->P)
+      return fail(GK_E_ARG, "stream %lld: bad table / pending sizes (pending <= n %% %d)", (long long)s, h->P);
   parallel_for(h->S, h->threads, [&](int64_t s) {
     Stream& st = h->st[s];
     st.n = n[s];

@@ -854,12 +854,15 @@ int gk_quantiles(gk_set* h, const double* qs, int nq, double* out, int mode, voi
   int rc = check_set(h);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
+  // settle the previous call first: a deferred stream of it is re-run with
+  // that call's query (h->last.q reads d_qs), which the upload below replaces
+  rc = grow_pools(h, s);
+  if (rc) return rc;
   GKQuery q;
   rc = prepare_query(h, qs, nq, out, mode, s, &q);
   if (rc) return rc;
   if (nq == 0 || h->S == 0) return GK_OK;
-  rc = grow_pools(h, s);
-  if (!rc) rc = take_sticky(h);
+  rc = take_sticky(h);
   if (!rc) rc = begin_call(h, s);
   if (rc) return rc;
   // gk:197-198: pending values are flushed first (state mutation); the
@@ -876,13 +879,14 @@ int gk_ingest_quantiles(gk_set* h, const double* values, const int64_t* offsets,
   if (!offsets) return fail(GK_E_ARG, "offsets is null");
   if (!values) return fail(GK_E_ARG, "values is null");
   hipStream_t s = (hipStream_t)stream;
+  rc = grow_pools(h, s);  // before d_qs is rewritten (see gk_quantiles)
+  if (rc) return rc;
   GKQuery q;
   rc = prepare_query(h, qs, nq, out, mode, s, &q);
   if (rc) return rc;
   if (h->S == 0) return GK_OK;
   if (nq == 0) return gk_ingest(h, values, offsets, stream);
-  rc = grow_pools(h, s);
-  if (!rc) rc = take_sticky(h);
+  rc = take_sticky(h);
   if (!rc) rc = begin_call(h, s);
   if (rc) return rc;
   rc = stats_fork(h, values, offsets, s);
@@ -898,6 +902,8 @@ int gk_ingest_quantiles(gk_set* h, const double* values, const int64_t* offsets,
 int gk_stats(gk_set* h, int64_t* n, double* mn, double* mx, double* sum, double* avg, int32_t* table_size,
              int32_t* pending, void* stream) {
   int rc = check_set(h);
+  if (rc) return rc;
+  rc = settle(h, (hipStream_t)stream, false);  // a deferred stream of the last call is re-run first
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   const int64_t S = h->S;
@@ -971,6 +977,8 @@ int gk_merge_compress(gk_set* h, const double* v, const int32_t* g, const int32_
 int gk_export_sizes(gk_set* h, int32_t* sizes, void* stream) {
   int rc = check_set(h);
   if (rc) return rc;
+  rc = settle(h, (hipStream_t)stream, false);  // a deferred stream of the last call is re-run first
+  if (rc) return rc;
   if (!sizes) return fail(GK_E_ARG, "sizes is null");
   if (h->S)
     HIP_TRY(hipMemcpyAsync(sizes, h->st.E, h->S * sizeof(int32_t), hipMemcpyDeviceToDevice, (hipStream_t)stream));
@@ -980,6 +988,8 @@ int gk_export_sizes(gk_set* h, int32_t* sizes, void* stream) {
 int gk_export(gk_set* h, const int64_t* offs, double* v, int32_t* g, int32_t* d, void* stream) {
   int rc = check_set(h);
   if (rc) return rc;
+  rc = settle(h, (hipStream_t)stream, false);  // a deferred stream of the last call is re-run first
+  if (rc) return rc;
   if (!offs) return fail(GK_E_ARG, "offs is null");
   HIP_TRY(gk_launch_export(h->st, offs, v, g, d, (hipStream_t)stream));
   return GK_OK;
@@ -987,6 +997,8 @@ int gk_export(gk_set* h, const int64_t* offs, double* v, int32_t* g, int32_t* d,
 
 int gk_export_pending_sizes(gk_set* h, int32_t* sizes, void* stream) {
   int rc = check_set(h);
+  if (rc) return rc;
+  rc = settle(h, (hipStream_t)stream, false);  // a deferred stream of the last call is re-run first
   if (rc) return rc;
   if (!sizes) return fail(GK_E_ARG, "sizes is null");
   if (h->S)
@@ -996,6 +1008,8 @@ int gk_export_pending_sizes(gk_set* h, int32_t* sizes, void* stream) {
 
 int gk_export_pending(gk_set* h, const int64_t* poffs, double* pv, void* stream) {
   int rc = check_set(h);
+  if (rc) return rc;
+  rc = settle(h, (hipStream_t)stream, false);  // a deferred stream of the last call is re-run first
   if (rc) return rc;
   if (!poffs || !pv) return fail(GK_E_ARG, "null pointer");
   HIP_TRY(gk_launch_export_pending(h->st, poffs, pv, (hipStream_t)stream));
@@ -1013,6 +1027,16 @@ int gk_import(gk_set* h, const int64_t* offs, const double* v, const int32_t* g,
   if (S == 0) return GK_OK;
   rc = gk_sync(h, stream);
   if (rc) return rc;
+  {
+    int32_t* bad = h->d_ctr + GK_CTR_BADPEND;
+    HIP_TRY(hipMemsetAsync(bad, 0, sizeof(int32_t), s));
+    HIP_TRY(gk_launch_check_pending(S, h->P, n, poffs, bad, s));
+    HIP_TRY(hipMemcpyAsync(h->h_ovf, bad, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (h->h_ovf[0] != 0)
+      return fail(GK_E_ARG, "%d stream(s) hold more pending values than add() leaves (pending <= n %% %d)",
+                  h->h_ovf[0], h->P);
+  }
   HIP_TRY(hipMemcpyAsync(h->st.n, n, S * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
   HIP_TRY(hipMemcpyAsync(h->st.mn, mn, S * sizeof(double), hipMemcpyDeviceToDevice, s));
   HIP_TRY(hipMemcpyAsync(h->st.mx, mx, S * sizeof(double), hipMemcpyDeviceToDevice, s));
@@ -1141,8 +1165,9 @@ int gk_load(gk_set* h, const char* path, void* stream) {
   for (int64_t k = 0; k < S; ++k) {
     offs[k + 1] = offs[k] + st.sizes[k];
     poffs[k + 1] = poffs[k] + st.psizes[k];
-    if (st.psizes[k] >= h->P) return fail(GK_E_FORMAT, "%s: stream %lld holds %d pending values (flush period %d)",
-                                          path, (long long)k, st.psizes[k], h->P);
+    if (st.psizes[k] < 0 || st.n[k] < 0 || st.psizes[k] > st.n[k] % h->P)
+      return fail(GK_E_FORMAT, "%s: stream %lld holds %d pending values at n=%lld (at most n mod %d)", path,
+                  (long long)k, st.psizes[k], (long long)st.n[k], h->P);
   }
   const int64_t E = offs[S], P = poffs[S];
   DevBuf d_offs, d_poffs, d_v, d_g, d_d, d_pv, d_hdr;
@@ -1234,6 +1259,7 @@ int64_t gk_num_promoted(const gk_set* h) {
   if (!h) return -1;
   if (h->S == 0) return 0;
   if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (settle(const_cast<gk_set*>(h), nullptr, true) != GK_OK) return -1;  // deferred streams placed first
   std::vector<int32_t> cls(h->S);
   if (hipMemcpy(cls.data(), h->st.cls, h->S * sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess) return -1;
   int64_t n = 0;

@@ -3297,6 +3297,19 @@ __global__ void k_export_pending(GKState st, const int64_t* __restrict__ offs, d
   }
 }
 
+// gk_import's argument check, before any state is written: a stream's
+// pending count p must be one that add() can leave behind -- the values added
+// since n last crossed a multiple of P (gk:60), so p <= n mod P (and p = 0
+// when n mod P = 0).  A flush batch is then at most P values.
+__global__ void k_check_pending(int64_t S, int P, const int64_t* __restrict__ n, const int64_t* __restrict__ poffs,
+                                int32_t* __restrict__ bad) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S) return;
+  const int64_t p = poffs[s + 1] - poffs[s];
+  const int64_t ns = n[s];
+  if (p < 0 || ns < 0 || p > ns % P) atomicAdd(bad, 1);
+}
+
 __global__ void k_import(GKState st, const int64_t* __restrict__ offs, const double* __restrict__ v,
                          const int32_t* __restrict__ g, const int32_t* __restrict__ d,
                          const int64_t* __restrict__ poffs, const double* __restrict__ pv,
@@ -3678,6 +3691,13 @@ hipError_t gk_launch_export(const GKState& st, const int64_t* offs, double* v, i
 hipError_t gk_launch_export_pending(const GKState& st, const int64_t* offs, double* v, hipStream_t stream) {
   if (st.S <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_export_pending, dim3((unsigned)wave_grid(st.S)), dim3(256), 0, stream, st, offs, v);
+  return hipGetLastError();
+}
+
+hipError_t gk_launch_check_pending(int64_t S, int P, const int64_t* n, const int64_t* poffs, int32_t* bad,
+                                  hipStream_t stream) {
+  if (S <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_check_pending, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, stream, S, P, n, poffs, bad);
   return hipGetLastError();
 }
 

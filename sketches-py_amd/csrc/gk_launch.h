@@ -108,6 +108,9 @@ hipError_t gk_launch_rtab(const GKState& st, hipStream_t stream);
 hipError_t gk_launch_export(const GKState& st, const int64_t* offs, double* v, int32_t* g, int32_t* d,
                             hipStream_t stream);
 hipError_t gk_launch_export_pending(const GKState& st, const int64_t* offs, double* v, hipStream_t stream);
+// counts into *bad the streams whose pending count p is not one add() can leave (p > n mod P)
+hipError_t gk_launch_check_pending(int64_t S, int P, const int64_t* n, const int64_t* poffs, int32_t* bad,
+                                  hipStream_t stream);
 hipError_t gk_launch_import(const GKState& st, const int64_t* offs, const double* v, const int32_t* g,
                             const int32_t* d, const int64_t* poffs, const double* pv, int32_t* ovf_count,
                             int32_t* ovf_list, hipStream_t stream);
@@ -133,6 +136,7 @@ hipError_t gk_launch_promote(const GKState& st, const int32_t* list, int64_t cou
 #define GK_CTR_LONG 15    // streams longer than GK_STATS_LONG values (k_stats)
 #define GK_CTR_RCNT 16    // [16 + 4*round + class]
 #define GK_CTR_OVFC 40    // [40 + round]
+#define GK_CTR_BADPEND 48 // gk_import: streams with an unreachable pending count
 #define GK_CTR_WORDS 16
 #define GK_CTR_CALL 14
 #define GK_CALL_WORK 256                          // bytes: the small-class launch's GK_WORK_BYTES, then

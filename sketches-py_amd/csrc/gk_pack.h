@@ -176,6 +176,24 @@ int read_header(gk_set* dst, const void* buf, Header* h, void* stream, std::stri
           std::to_string(gk_num_streams(dst));
     return GK_E_ARG;
   }
+  // sizes and offsets: a truncated or corrupt buffer must not reach gk_import
+  // (whose copies would read past the buffer)
+  if (h->E < 0 || h->P < 0 || h->E > ((int64_t)1 << 40) || h->P > ((int64_t)1 << 40) ||
+      h->bytes != (int64_t)layout(h->S, h->E, h->P).total) {
+    err = "packed state header is inconsistent (sizes / byte count)";
+    return GK_E_FORMAT;
+  }
+  const Layout L = layout(h->S, h->E, h->P);
+  std::vector<int64_t> eo(h->S + 1), po(h->S + 1);
+  rc = Mem::to_host(eo.data(), at<int64_t>(buf, L.eoffs), 8 * (size_t)(h->S + 1), stream);
+  if (!rc) rc = Mem::to_host(po.data(), at<int64_t>(buf, L.poffs), 8 * (size_t)(h->S + 1), stream);
+  if (rc) return rc;
+  bool ok = eo[0] == 0 && po[0] == 0 && eo[h->S] == h->E && po[h->S] == h->P;
+  for (int64_t s = 0; ok && s < h->S; ++s) ok = eo[s + 1] >= eo[s] && po[s + 1] >= po[s];
+  if (!ok) {
+    err = "packed state offsets are not monotone from 0 to the header's totals";
+    return GK_E_FORMAT;
+  }
   return GK_OK;
 }
 

@@ -81,10 +81,15 @@ class GKArray:
         """The stream's table := recs [(v, g, delta)], pending := values
         (header words kept): one gk_import."""
         P = self._set.flush_period
-        if len(pending) >= P:
-            raise ValueError("incoming holds %d values; at most %d fit the flush period" % (len(pending), P - 1))
         dev = self._set.device
         st = self._set.stats()
+        # add() leaves at most n mod P values pending (gk:60): the values added
+        # since n last crossed a multiple of P; a longer list has no flush
+        # schedule in this engine (one flush batch is at most P values)
+        room = int(st["n"][0].item()) % P
+        if len(pending) > room:
+            raise ValueError("incoming holds %d values; at n=%d at most %d can be pending (n mod %d)"
+                             % (len(pending), int(st["n"][0].item()), room, P))
         f64 = lambda a: torch.tensor(a if a else [0.0], dtype=torch.float64, device=dev)
         i32 = lambda a: torch.tensor(a if a else [0], dtype=torch.int32, device=dev)
         i64 = lambda a: torch.tensor(a, dtype=torch.int64, device=dev)

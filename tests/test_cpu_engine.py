@@ -279,3 +279,63 @@ def test_packed_state_round_trip_and_fold():
         StreamSet(S + 1, eps, device=CPU).fold_packed(bufs[:1])
     with pytest.raises(GKBackendError):
         sets[0].pack(torch.zeros(16, dtype=torch.uint8))
+
+
+def test_packed_state_corrupt_header_and_offsets_refused():
+    """a packed buffer whose header sizes / byte count or
+    offset arrays are inconsistent is refused before gk_import reads it."""
+    from gkarray_amd import StreamSet
+    from gkarray_amd._lib import GKBackendError
+    rng = np.random.default_rng(18)
+    eps, S = 0.01, 12
+    seqs = [gen(int(rng.integers(0, 8)), int(rng.integers(1, 500)), rng) for _ in range(S)]
+    flat, offs = csr(seqs)
+    ss = StreamSet(S, eps, device=CPU)
+    ss.ingest(torch.from_numpy(flat), torch.from_numpy(offs))
+    good = ss.pack()
+    StreamSet(S, eps, device=CPU).fold_packed([good])  # sanity: the intact buffer folds
+    hdr = good[:64].numpy().view(np.int64)  # magic, version|hbytes, eps, S, E, P, bytes, reserved
+    for field, val in ((4, -1), (4, int(hdr[4]) + 1), (5, -3), (6, int(hdr[6]) - 256)):
+        bad = good.clone()
+        bad[:64].numpy().view(np.int64)[field] = val
+        with pytest.raises(GKBackendError):
+            StreamSet(S, eps, device=CPU).fold_packed([bad])
+    # a non-monotone table offset array (section at 256-aligned offset after 5 header arrays)
+    sec = lambda nbytes: (nbytes + 255) // 256 * 256
+    eoffs_at = 256 + 5 * sec(8 * S)
+    bad = good.clone()
+    eo = bad[eoffs_at:eoffs_at + 8 * (S + 1)].numpy().view(np.int64)
+    eo[3], eo[4] = eo[4] + 1, eo[3]
+    with pytest.raises(GKBackendError, match="offsets"):
+        StreamSet(S, eps, device=CPU).fold_packed([bad])
+
+
+def test_import_rejects_unreachable_pending_cpu():
+    """pending counts above n mod P are refused by the host
+    engine's import too (and by the drop-in's incoming assignment)."""
+    from gkarray_amd import GKArray, StreamSet
+    from gkarray_amd._lib import GKBackendError
+    eps, S = 0.01, 3
+    P = int(1 / eps) + 1
+    rng = np.random.default_rng(19)
+    seqs = [rng.random(2 * P + 4) for _ in range(S)]
+    flat, offs = csr(seqs)
+    ss = StreamSet(S, eps, device=CPU)
+    ss.ingest(torch.from_numpy(flat), torch.from_numpy(offs))
+    st = ss.export_state()
+    bad = dict(st)
+    bad["poffs"] = torch.tensor([0, 4, 14, 18], dtype=torch.int64)  # 10 pending at n mod P = 4
+    bad["pv"] = torch.rand(18, dtype=torch.float64)
+    with pytest.raises(GKBackendError, match="pending"):
+        ss.import_state(bad)
+    sk = GKArray(eps, device=CPU)
+    for x in rng.random(P):  # n = P: just flushed, nothing can be pending
+        sk.add(float(x))
+    with pytest.raises(ValueError, match="pending"):
+        sk.incoming = [0.5] * 28
+        sk.size()
+    sk2 = GKArray(eps, device=CPU)
+    for x in rng.random(P + 30):
+        sk2.add(float(x))
+    sk2.incoming = [0.25] * 30  # n mod P = 30: allowed
+    assert sk2.size() > 0

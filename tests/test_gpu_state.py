@@ -180,3 +180,82 @@ def test_packed_states_fold_on_gpu(gpu_device, eps):
     o1 = OracleSet(S, eps)
     o1.ingest(*flats[1])
     assert_same_state(g2, o1, "host-packed on gpu")
+
+
+def _deferring_batch(S, rng):
+    """Streams that outgrow the small class (descending runs): with 2 arena
+    slots (GK_POOL_SLOTS) most of them are deferred and re-run later."""
+    seqs = [np.sort(rng.random(int(L)))[::-1].copy() if k % 3 else rng.random(int(L))
+            for k, L in enumerate(rng.integers(5000, 30000, S))]
+    return csr(seqs)
+
+
+def test_deferred_query_keeps_its_own_qs(gpu_device, monkeypatch):
+    """a fused ingest+quantiles call left in flight (sync=False)
+    with deferred streams, then quantiles() with a longer q list (> 64: the
+    device q buffer is reallocated).  The deferred streams of the first call
+    are re-run with the FIRST call's q values into the first output; both
+    outputs equal the oracle's."""
+    monkeypatch.setenv("GK_POOL_SLOTS", "2")
+    rng = np.random.default_rng(85)
+    S = 48
+    ss = _ss(S, 0.01, gpu_device)
+    o = OracleSet(S, 0.01)
+    flat, offs = _deferring_batch(S, rng)
+    tf, to = torch.from_numpy(flat).to(gpu_device), torch.from_numpy(offs).to(gpu_device)
+    q1 = [0.5, 0.9]
+    out1 = ss.ingest(tf, to, quantiles=q1, sync=False)
+    q2 = [float(x) for x in np.linspace(0.0, 1.0, 70)]
+    out2 = ss.quantiles(q2)
+    o.ingest(flat, offs)
+    e1 = o.quantiles(q1)
+    e2 = o.quantiles(q2)
+    assert ss.num_promoted > 2
+    assert_same_quantiles(out1.cpu().numpy(), e1, "first (deferred) query", small_of(o, 0.01))
+    assert_same_quantiles(out2.cpu().numpy(), e2, "second query", small_of(o, 0.01))
+    assert_same_state(ss, o, "after both queries")
+
+
+def test_export_after_async_ingest_sees_deferred_streams(gpu_device, monkeypatch):
+    """reads of the state (stats, sizes, tables, pending) right
+    after ingest(sync=False) first re-run the call's deferred streams, so an
+    export never mixes a deferred stream's old table with its new header."""
+    monkeypatch.setenv("GK_POOL_SLOTS", "2")
+    rng = np.random.default_rng(86)
+    S = 48
+    ss = _ss(S, 0.01, gpu_device)
+    o = OracleSet(S, 0.01)
+    flat, offs = _deferring_batch(S, rng)
+    tf, to = torch.from_numpy(flat).to(gpu_device), torch.from_numpy(offs).to(gpu_device)
+    ss.ingest(tf, to, sync=False)
+    st = ss.export_state()  # no sync() in between
+    o.ingest(flat, offs)
+    o_off, o_v, o_g, o_d = o.tables()
+    assert np.array_equal(st["offs"].cpu().numpy(), o_off)
+    assert np.array_equal(st["v"].cpu().numpy().view(np.int64), np.asarray(o_v).view(np.int64))
+    assert np.array_equal(st["g"].cpu().numpy(), o_g) and np.array_equal(st["d"].cpu().numpy(), o_d)
+    ost = o.stats()
+    assert np.array_equal(st["n"].cpu().numpy(), ost["n"])
+
+
+def test_import_rejects_unreachable_pending(gpu_device):
+    """a state whose pending count exceeds n mod P (no sequence
+    of adds leaves it; its flush batch would exceed P values) is refused
+    before anything is written; the set keeps its state."""
+    from gkarray_amd import GKBackendError
+    S, eps = 4, 0.01
+    P = int(1 / eps) + 1
+    rng = np.random.default_rng(87)
+    seqs = [rng.random(3 * P + 5) for _ in range(S)]
+    ss = _ss(S, eps, gpu_device)
+    flat, offs = csr(seqs)
+    ss.ingest(torch.from_numpy(flat), torch.from_numpy(offs))
+    o = OracleSet(S, eps)
+    o.ingest(flat, offs)
+    st = ss.export_state()
+    bad = dict(st)
+    bad["poffs"] = torch.tensor([0, 5, 35, 40, 45], dtype=torch.int64)  # stream 1: 30 pending at n mod P = 5
+    bad["pv"] = torch.rand(45, dtype=torch.float64)
+    with pytest.raises(GKBackendError, match="pending"):
+        ss.import_state(bad)
+    assert_same_state(ss, o, "untouched after the refused import")
