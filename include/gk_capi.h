@@ -28,8 +28,8 @@
  *    gk_merge,
  *    gk_merge_compress, gk_import, gk_save / gk_load and gk_num_promoted
  *    synchronise before returning.
- *  - Limits.  Any eps with int(1/eps)+1 < 2^24 is accepted (the reference:
- *    any eps); tables grow through capacity classes up to 2^27 entries per
+ *  - Limits.  Any finite eps > 0 with int(1/eps)+1 < 2^24 is accepted (the
+ *    reference: any eps; eps > 1 gives a flush period of 1, gk:60); tables grow through capacity classes up to 2^27 entries per
  *    stream (the last classes are allocated on first use).  One stream may
  *    hold n values while 2*eps*(n-1) <= 2^30 (5.4e10 values at eps=0.01):
  *    its tuples' g and delta are int32 (GKRec).

@@ -8,7 +8,7 @@
  *  - `stream` arguments are ignored (all calls are synchronous, gk_sync is a
  *    no-op), `device` of gk_create is ignored;
  *  - there are no capacity classes: tables and pending buffers grow without
- *    bound, any eps in (0, 1] is accepted, GK_E_OVERFLOW never occurs;
+ *    bound, any finite eps > 0 is accepted, GK_E_OVERFLOW never occurs;
  *  - streams are processed in parallel on host threads (each stream strictly
  *    in insertion order): GK_CPU_THREADS (environment) or gk_cpu_set_threads,
  *    default = the CPUs this process may run on.

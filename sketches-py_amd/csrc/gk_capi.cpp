@@ -573,7 +573,8 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
   if (!out) return fail(GK_E_ARG, "out is null");
   *out = nullptr;
   if (num_streams < 0 || num_streams > INT32_MAX) return fail(GK_E_ARG, "num_streams out of range");
-  if (std::isnan(eps) || !(eps > 0.0) || !(eps <= 1.0)) return fail(GK_E_ARG, "eps must be in (0, 1]");
+  // any finite eps > 0, as the reference (gk:21); eps > 1 gives P = 1 (gk:60)
+  if (!std::isfinite(eps) || !(eps > 0.0)) return fail(GK_E_ARG, "eps must be finite and > 0");
   const double inv = 1.0 / eps;
   if (inv >= (double)kPMax)
     return fail(GK_E_UNSUPPORTED, "eps=%g: flush period int(1/eps)+1 beyond %d is not supported", eps, kPMax);

@@ -288,6 +288,31 @@ def main():
     kat["kat3_stats"] = stats(sk)
     kat["kat3_table"] = snap(sk)
 
+    # -- 6. eps > 1 (gk:21 accepts any eps; gk:60 gives P = int(1/eps)+1 = 2
+    #       at eps = 1 and 1 above it: every add flushes) -- appended last so
+    #       that the cases above keep their ids and random draws
+    rng6 = np.random.default_rng(20261017)
+    for eps in [1.0, 1.5, 3.0]:
+        for dist in ["uniform", "pareto", "descending", "fewdistinct", "zeros"]:
+            for L in [1, 2, 3, 7, 60, 400]:
+                xs = gen_values(dist, L, rng6)
+                run_stream_case(ref, st, cid, eps, xs, per_flush=True)
+                st.index.append(dict(id=cid, kind="stream", eps=eps, dist=dist, L=int(L)))
+                cid += 1
+        for dist in ["uniform", "zeros"]:
+            L = 40
+            xs = gen_values(dist, L, rng6)
+            run_query_mid_case(ref, st, cid, eps, xs, [1, 2, 5, 17, 39])
+            st.index.append(dict(id=cid, kind="query_mid", eps=eps, dist=dist, L=int(L)))
+            cid += 1
+        for k in [2, 3]:
+            lens = rng6.integers(0, 120, k)
+            lens[0] = max(lens[0], 1)
+            shards = [gen_values("lognormal", int(L), rng6) for L in lens]
+            run_merge_case(ref, st, cid, eps, shards)
+            st.index.append(dict(id=cid, kind="merge", eps=eps, dist="lognormal", k=k))
+            cid += 1
+
     np.savez_compressed(os.path.join(HERE, "golden.npz"), **st.arrays)
     with open(os.path.join(HERE, "golden_index.json"), "w") as f:
         json.dump(dict(cases=st.index, kat=kat, qs=QS, qs_unsorted=QS_UNSORTED,
