@@ -38,6 +38,44 @@ _I64 = ("offs", "poffs", "n")
 _I32 = ("g", "d")
 
 
+def _host_staged(t, group=None):
+    """True when the group's backend cannot move tensors of t's device: gloo
+    with device tensors (a rehearsal of the N-rank path on one GPU, or CPU
+    tests).  RCCL ("nccl") moves device tensors directly."""
+    return t.device.type != "cpu" and dist.get_backend(group) == "gloo"
+
+
+def _all_gather(out, t, group=None):
+    """dist.all_gather into `out` (a list of tensors shaped like t); over gloo
+    device tensors are staged through host memory."""
+    if not _host_staged(t, group):
+        dist.all_gather(out, t, group=group)
+        return
+    tc = t.cpu()
+    oc = [torch.empty_like(tc) for _ in out]
+    dist.all_gather(oc, tc, group=group)
+    for o, c in zip(out, oc):
+        o.copy_(c)
+
+
+def _all_to_all_single(out, inp, out_splits=None, in_splits=None, group=None):
+    if not _host_staged(inp, group):
+        dist.all_to_all_single(out, inp, output_split_sizes=out_splits, input_split_sizes=in_splits, group=group)
+        return
+    oc = torch.empty(out.shape, dtype=out.dtype)
+    dist.all_to_all_single(oc, inp.cpu(), output_split_sizes=out_splits, input_split_sizes=in_splits, group=group)
+    out.copy_(oc)
+
+
+def _all_reduce(t, op, group=None):
+    if not _host_staged(t, group):
+        dist.all_reduce(t, op=op, group=group)
+        return
+    c = t.cpu()
+    dist.all_reduce(c, op=op, group=group)
+    t.copy_(c)
+
+
 def stream_range(S, world, rank):
     """Contiguous, balanced stream range [a, b) of `rank` out of `world`."""
     q, r = divmod(S, world)
@@ -85,13 +123,13 @@ def all_gather_varlen(t, group=None):
     world = dist.get_world_size(group)
     n = torch.tensor([t.numel()], dtype=torch.int64, device=t.device)
     sizes = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(sizes, n, group=group)
+    _all_gather(sizes, n, group=group)
     sizes = [int(s.item()) for s in sizes]
     m = max(sizes) if sizes else 0
     pad = torch.zeros(m, dtype=t.dtype, device=t.device)
     pad[:t.numel()] = t
     bufs = [torch.empty(m, dtype=t.dtype, device=t.device) for _ in range(world)]
-    dist.all_gather(bufs, pad, group=group)
+    _all_gather(bufs, pad, group=group)
     return [b[:s] for b, s in zip(bufs, sizes)]
 
 
@@ -122,14 +160,13 @@ def alltoall_states(state, group=None):
                         dtype=torch.int64, device=dev)
     flat_in = meta.reshape(-1).contiguous()
     flat_out = torch.empty_like(flat_in)
-    dist.all_to_all_single(flat_out, flat_in, group=group)
+    _all_to_all_single(flat_out, flat_in, group=group)
     rmeta = flat_out.reshape(world, 3 + nlen).cpu()
     out = []
     for k in range(3):
         src = torch.cat([p[k] for p in parts])
         recv = torch.empty(int(rmeta[:, k].sum()), dtype=src.dtype, device=dev)
-        dist.all_to_all_single(recv, src, output_split_sizes=rmeta[:, k].tolist(),
-                               input_split_sizes=[int(p[k].numel()) for p in parts], group=group)
+        _all_to_all_single(recv, src, rmeta[:, k].tolist(), [int(p[k].numel()) for p in parts], group=group)
         out.append(list(torch.split(recv, rmeta[:, k].tolist())))
     return [unpack_state(out[0][r], out[1][r], out[2][r], [int(x) for x in rmeta[r, 3:].tolist()], state["eps"])
             for r in range(world)]
@@ -250,7 +287,7 @@ class RowShardMerger:
         if self.world == 1:
             return [t]
         out = [torch.empty_like(t) for _ in range(self.world)]
-        dist.all_gather(out, t, group=self.group)
+        _all_gather(out, t, group=self.group)
         return out
 
     def __call__(self, ss):
@@ -337,12 +374,9 @@ class RowShardMerger:
         f_recv = torch.empty(sum(f_out_sizes), dtype=torch.float64, device=dev)
         i_recv = torch.empty(sum(i_out_sizes), dtype=torch.int64, device=dev)
         j_recv = torch.empty(max(sum(j_out_sizes), 1), dtype=torch.int32, device=dev)
-        dist.all_to_all_single(f_recv, f_send, output_split_sizes=f_out_sizes, input_split_sizes=f_in_sizes,
-                               group=self.group)
-        dist.all_to_all_single(i_recv, i_send, output_split_sizes=i_out_sizes, input_split_sizes=i_in_sizes,
-                               group=self.group)
-        dist.all_to_all_single(j_recv[:sum(j_out_sizes)], j_send, output_split_sizes=j_out_sizes,
-                               input_split_sizes=j_in_sizes, group=self.group)
+        _all_to_all_single(f_recv, f_send, f_out_sizes, f_in_sizes, group=self.group)
+        _all_to_all_single(i_recv, i_send, i_out_sizes, i_in_sizes, group=self.group)
+        _all_to_all_single(j_recv[:sum(j_out_sizes)], j_send, j_out_sizes, j_in_sizes, group=self.group)
         views = []
         fo = io = jo = 0
         m = b - a
@@ -365,11 +399,11 @@ def allgather_packed(ss, group=None):
     of that size, one all-gather moves them."""
     dev = ss.device
     n = torch.tensor([ss.pack_bytes()], dtype=torch.int64, device=dev)
-    dist.all_reduce(n, op=dist.ReduceOp.MAX, group=group)
+    _all_reduce(n, dist.ReduceOp.MAX, group=group)
     buf = torch.zeros(int(n.item()), dtype=torch.uint8, device=dev)
     ss.pack(buf)
     out = [torch.empty_like(buf) for _ in range(dist.get_world_size(group))]
-    dist.all_gather(out, buf, group=group)
+    _all_gather(out, buf, group=group)
     return out
 
 

@@ -198,8 +198,9 @@ def _merger_worker(rank, world, port, S, eps, exchange, q):
             m = merger(ss)
             to, v, g, d = (t.clone() for t in m.tables())
             st = {k: t.clone() for k, t in m.stats().items()}
-            res = (to.tolist(), v.tolist(), g.tolist(), d.tolist(), st["n"].tolist(), st["min"].tolist(),
-                   st["max"].tolist())
+            bits = lambda t: t.contiguous().view(torch.int64).tolist()  # float64 bit patterns (+0.0 != -0.0)
+            res = (to.tolist(), bits(v), g.tolist(), d.tolist(), st["n"].tolist(), bits(st["min"]),
+                   bits(st["max"]))
         q.put((rank, merger.range, res))
     finally:
         dist.destroy_process_group()
@@ -228,13 +229,15 @@ def test_gloo_row_shard_merger(world, exchange):
         ref.merge(o)
     ro, rv, rg, rd = ref.tables()
     rst = ref.stats()
+    rvb = np.ascontiguousarray(rv).view(np.int64)
+    rmn, rmx = rst["min"].view(np.int64), rst["max"].view(np.int64)
     covered = []
     for rank, (a, b), (to, v, g, d, n, mn, mx) in sorted(results):
         for k, s in enumerate(range(a, b)):
-            exp = list(zip(rv[ro[s]:ro[s + 1]].tolist(), rg[ro[s]:ro[s + 1]].tolist(), rd[ro[s]:ro[s + 1]].tolist()))
+            exp = list(zip(rvb[ro[s]:ro[s + 1]].tolist(), rg[ro[s]:ro[s + 1]].tolist(), rd[ro[s]:ro[s + 1]].tolist()))
             got = list(zip(v[to[k]:to[k + 1]], g[to[k]:to[k + 1]], d[to[k]:to[k + 1]]))
             assert got == exp, (rank, s)
-            assert n[k] == rst["n"][s] and mn[k] == rst["min"][s] and mx[k] == rst["max"][s]
+            assert n[k] == rst["n"][s] and mn[k] == rmn[s] and mx[k] == rmx[s]
         covered.extend(range(a, b))
     assert covered == list(range(S))
 
@@ -253,8 +256,9 @@ def _packed_worker(rank, world, port, S, eps, q):
         to, v, g, d = dst.tables()
         st = dst.stats()
         po, pv = dst.pending()
-        q.put((rank, (to.tolist(), v.tolist(), g.tolist(), d.tolist(), st["n"].tolist(), st["min"].tolist(),
-                      st["max"].tolist(), st["sum"].tolist(), po.tolist(), pv.tolist())))
+        bits = lambda t: t.contiguous().view(torch.int64).tolist()  # float64 bit patterns (+0.0 != -0.0)
+        q.put((rank, (to.tolist(), bits(v), g.tolist(), d.tolist(), st["n"].tolist(), bits(st["min"]),
+                      bits(st["max"]), bits(st["sum"]), po.tolist(), bits(pv))))
     finally:
         dist.destroy_process_group()
 
@@ -284,8 +288,9 @@ def test_gloo_fold_packed_allgather(world):
     ro, rv, rg, rd = ref.tables()
     rst = ref.stats()
     rpo, rpv = ref.pending()
+    b = lambda a: np.ascontiguousarray(a, dtype=np.float64).view(np.int64).tolist()
     for rank, (to, v, g, d, n, mn, mx, sm, po, pv) in results:
-        assert to == ro.tolist() and v == rv.tolist() and g == rg.tolist() and d == rd.tolist(), rank
-        assert n == rst["n"].tolist() and mn == rst["min"].tolist() and mx == rst["max"].tolist(), rank
-        assert sm == rst["sum"].tolist(), rank
-        assert po == rpo.tolist() and pv == rpv.tolist(), rank
+        assert to == ro.tolist() and v == b(rv) and g == rg.tolist() and d == rd.tolist(), rank
+        assert n == rst["n"].tolist() and mn == b(rst["min"]) and mx == b(rst["max"]), rank
+        assert sm == b(rst["sum"]), rank
+        assert po == rpo.tolist() and pv == b(rpv), rank
