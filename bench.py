@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="0 = the CPUs this process may use (capped by OMP_NUM_THREADS if set)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-all-cores", action="store_true",
+                    help="also time the host engine on every CPU of the affinity set (beyond this job's share)")
     ap.add_argument("--exchange", default="allgather", choices=["allgather", "alltoall"],
                     help="cfg4 row-shard exchange over RCCL before the merge fold")
     ap.add_argument("--virtual-shards", type=int, default=1,
@@ -140,14 +142,24 @@ def host_cores():
     return threads, aff, os.cpu_count() or aff
 
 
-def cpu_baseline(x, offs, sample, threads, eps, gpu_q, py_streams=2000):
+# gkarray.py itself (Entry objects), cfg3 shape, 1 process per core, measured in
+# the build container (BASELINE.md / SURVEY 6); the reference never travels to
+# the GPU box, so it is quoted, not re-timed here
+REFERENCE_CFG3_RATE = {"1core": 529e3, "8cores": 3.59e6}
+
+
+def cpu_baseline(x, offs, sample, threads, eps, gpu_q, py_streams=2000, all_cores=False):
     """The reference path on the host, timed on this box (rank 0, N=1):
     * the product's host engine (libgkarray_cpu.so, StreamSet(device="cpu"),
-      threads over streams) on the first `sample` streams of the same batch --
-      also a parity check of the GPU quantiles on that sample;
-    * the reference algorithm in pure Python on ONE core (oracle/gk_oracle.py,
-      test infrastructure, like-for-like with gkarray.py's own speed: SURVEY 6
-      measured 529k values/s/core) on the first `py_streams` streams."""
+      threads over streams) on the first `sample` streams of the same batch, on
+      the box's CPU share for this job (OMP_NUM_THREADS: 16 of the machine's
+      CPUs) -- also a parity check of the GPU quantiles on that sample; with
+      `all_cores` a second leg on every CPU of the affinity set (opt-in: the
+      box asks jobs to keep to their share);
+    * the reference algorithm restated over parallel lists (oracle/gk_oracle.py,
+      test infrastructure: no Entry objects, so ~3x faster than gkarray.py) on
+      ONE core on the first `py_streams` streams, beside gkarray.py's own rate
+      measured in the build container (REFERENCE_CFG3_RATE)."""
     from gkarray_amd import StreamSet
     o_all = offs[: sample + 1].cpu().numpy()
     nv = int(o_all[-1] - o_all[0])
@@ -171,14 +183,35 @@ def cpu_baseline(x, offs, sample, threads, eps, gpu_q, py_streams=2000):
     dpy = time.perf_counter() - t1
     npy = int(o_all[ps] - o_all[0])
     _, aff, ncpu = host_cores()
-    return dict(value=nv / dt, unit="values/s", cores=threads, kind="port",
-                sample="%d streams, %d values (the first streams of the GPU workload), ingest + "
-                       "quantiles([.5,.9,.99]) in the host engine libgkarray_cpu.so on %d threads, %.2f s"
-                       % (sample, nv, threads, dt),
-                parity_on_sample=bool(same), host_cpus=ncpu, affinity_cpus=aff,
-                python_1core=dict(value=npy / dpy, unit="values/s", cores=1,
-                                  sample="%d streams, %d values, pure-Python restatement of gkarray.py "
-                                         "(oracle/gk_oracle.py), %.2f s" % (ps, npy, dpy)))
+    out = dict(value=nv / dt, unit="values/s", cores=threads, kind="port",
+               sample="%d streams, %d values (the first streams of the GPU workload), ingest + "
+                      "quantiles([.5,.9,.99]) in the host engine libgkarray_cpu.so on %d threads (this job's "
+                      "CPU share), %.2f s" % (sample, nv, threads, dt),
+               parity_on_sample=bool(same), host_cpus=ncpu, affinity_cpus=aff,
+               per_thread=nv / dt / threads,
+               python_1core=dict(value=npy / dpy, unit="values/s", cores=1,
+                                 sample="%d streams, %d values, the reference algorithm restated over parallel "
+                                        "lists in pure Python (oracle/gk_oracle.py: no Entry objects, ~3x "
+                                        "gkarray.py's speed), %.2f s" % (ps, npy, dpy)),
+               reference_gkarray_py=dict(value_1core=REFERENCE_CFG3_RATE["1core"],
+                                         value_8cores=REFERENCE_CFG3_RATE["8cores"], unit="values/s",
+                                         source="gkarray.py itself (Entry objects), cfg3 shape, 1 process per "
+                                                "core, measured in the build container (BASELINE.md, SURVEY 6); "
+                                                "quoted, the reference does not run on the GPU box"))
+    if all_cores and aff > threads:
+        hs.reset()
+        hs.set_threads(aff)
+        t2 = time.perf_counter()
+        hs.ingest(xs, o_loc, quantiles=[0.5, 0.9, 0.99])
+        d2 = time.perf_counter() - t2
+        out["all_cores"] = dict(value=nv / d2, unit="values/s", cores=aff,
+                                sample="same %d streams on every CPU of the affinity set, %.2f s" % (sample, d2))
+    else:
+        out["all_cores"] = dict(value=None, cores=aff, estimate=nv / dt / threads * aff,
+                                note="not run by default (the box allots %d CPUs to this job); estimate = "
+                                     "per-thread rate x %d CPUs, bench.py --cpu-all-cores measures it"
+                                     % (threads, aff))
+    return out
 
 
 def main():
@@ -341,7 +374,8 @@ def main():
         sample = min(a.cpu_sample, S)
         if a.workload == "cfg5":  # the long streams dominate: a bounded prefix of streams
             sample = min(sample, 20000)
-        line["cpu_baseline"] = cpu_baseline(x, offs, sample, threads, a.eps, q.cpu().numpy())
+        line["cpu_baseline"] = cpu_baseline(x, offs, sample, threads, a.eps, q.cpu().numpy(),
+                                            all_cores=a.cpu_all_cores)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

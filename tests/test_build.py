@@ -56,12 +56,12 @@ def test_fast_class_has_no_scratch(resource_report, small_isa):
     global addresses into scratch: stored once at kernel entry, reloaded once
     per stream (end-of-stream pending copy, the empty-table first flush).
     Keeping them in registers instead (e.g. re-reading the gap info at emit)
-    measured 1-2% slower (profiles/r01t_ab_regpressure_REJECTED.txt), so the
+    measured 1-2% slower (profiles/archive/r01t_ab_regpressure_REJECTED.txt), so the
     bound is on the count: a spill inside the flush loops adds many more.
     The stats role (fused_stats_role, run by a few waves before they join the
     hand-out) adds one more folded value (48 bytes, 11 scratch instructions
     at most); the ingest-only launch measured the same with and without it
-    (GK_FUSED_STATS=0 rows of profiles/r01z_ab_fused_stats.txt).
+    (GK_FUSED_STATS=0 rows of profiles/archive/r01z_ab_fused_stats.txt).
     The VPL=1 instance (P <= 64) carries more since the DPP lane exchanges
     (profiles/r02k_dpp_exchanges_sq.txt: one 4-byte reload per flush) and the
     paced stats role (per-batch reloads of its part bounds,
