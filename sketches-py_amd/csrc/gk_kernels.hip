@@ -2031,9 +2031,14 @@ __device__ __forceinline__ int gk_dma_flush_values(PrefetchLDS<VPL>& L, const do
 // gap counters of the next flush (gi[].x, read and written only inside a
 // flush): padded indices 0 .. pidx(127) = 130 of the SMALL_TVN = 136 records
 static_assert(SMALL_CAP + (SMALL_CAP >> 5) + 4 == 136, "gi zeroing covers 136 records");
+// (The zero is made at each use: hoisted out of the stream loop, the compiler
+// keeps a 4-VGPR zero alive across the flush and, short of registers, spills
+// it -- its reload's vmcnt wait then stalls on the in-flight LDS-DMA.)
 __device__ __forceinline__ void small_zero_counts(int2* gi, int lane) {
-  ((uint4*)gi)[lane] = make_uint4(0u, 0u, 0u, 0u);               // records 0..127
-  ((uint2*)gi)[128 + (lane & 7)] = make_uint2(0u, 0u);           // records 128..135
+  uint32_t z;
+  __asm__ volatile("v_mov_b32 %0, 0" : "=v"(z));
+  ((uint4*)gi)[lane] = make_uint4(z, z, z, z);           // records 0..127
+  ((uint2*)gi)[128 + (lane & 7)] = make_uint2(z, z);     // records 128..135
 }
 
 __device__ __forceinline__ void small_pad(double* tv, int E, int lane) {
@@ -2097,9 +2102,9 @@ __device__ __forceinline__ void small_emit(SmallLDS<VPL>& L, bool in_gap, const 
   const int q = cd.div(rk);
   const int rr = cd.rem(rk, q);
   // gap: kept iff rk - k >= 0; tail: kept iff rr = cs-1 or rk = m-1 (both
-  // differences <= 0, so their min is 0 iff one of them is 0)
+  // differences <= 0, so their max is 0 iff one of them is 0)
   const int dg = rk - k;
-  const int dt = min(rr - (cd.cs - 1), rk - gi_m(gi.x) + 1);  // <= 0
+  const int dt = max(rr - (cd.cs - 1), rk - gi_m(gi.x) + 1);  // <= 0
   const int pos = gi_ob(gi.x) + (in_gap ? dg : q);
   const int drop = (in_gap ? dg : (dt >> 31)) | vi;  // < 0: not kept
   small_put(L, drop < 0 ? GK_SMALL_TRASH : pos, x, in_gap ? 1 : rr + 1, gi.y);
@@ -2937,7 +2942,11 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
         if (!((force == 1 && p + nadd > 0) || force == 2)) break;
       }
       const int cnt = p + (int)nadd;
+#ifdef GK_NO_DMA
+      if (false) {
+#else
       if (flushed || have_pf) {
+#endif
         // DMA'd during the previous flush (or the previous stream's last)
         __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
@@ -2946,13 +2955,21 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
       } else {
         gk_load_flush_values<VPL>(xv, pb, p, x ? x + xo + used : pb, cnt, lane);
       }
+#ifdef GK_NO_DMA
+      if (false)
+#endif
       next_step();  // (before any DMA of this flush: its waits are on older loads only)
       const int64_t nused = used + nadd;
       // the next flush's values: this stream's (if it flushes again: full
       // period, or a requested flush of the leftover), else the next stream's
       // first flush's
       const int64_t rest = autof ? Lx - nused : 0;
+#ifdef GK_NO_DMA
+      if (false) {
+      } else if (false) {
+#else
       if (rest > 0 && (rest >= P || force != 0)) {
+#endif
         pfsh = gk_dma_flush_values<VPL>(PF, pb, 0, x + xo + nused, (int)min((int64_t)P, rest), lane);
       } else if (nst == 3 && wn < count && (int32_t)__builtin_amdgcn_readlane(hn, 0) == 0) {
         const int np = (int)__builtin_amdgcn_readlane(hn, 2);
