@@ -249,30 +249,6 @@ __device__ __forceinline__ void gk_hdr_issue(GKHdrV& h, const GKState& st, const
   }
 }
 
-// Lane-distributed stream header: lane k loads 32-bit word k of
-// {cls, slot, pend, E, n (2 words), offs[s] (2), offs[s+1] (2), min (2),
-// max (2)}; one VGPR instead of a register per field (MINMAX false: lanes
-// 10.. re-read cls).
-template <bool MINMAX>
-__device__ __forceinline__ const uint32_t* hdr_lane_ptr(const GKState& st, const int64_t* offs, int64_t s, int lane) {
-  const uint32_t* p = (const uint32_t*)(st.cls + s);
-  p = lane == 1 ? (const uint32_t*)(st.slot + s) : p;
-  p = lane == 2 ? (const uint32_t*)(st.pend + s) : p;
-  p = lane == 3 ? (const uint32_t*)(st.E + s) : p;
-  p = (lane & ~1) == 4 ? (const uint32_t*)(st.n + s) + (lane & 1) : p;
-  p = (lane & ~1) == 6 ? (const uint32_t*)(offs + s) + (lane & 1) : p;
-  p = (lane & ~1) == 8 ? (const uint32_t*)(offs + s + 1) + (lane & 1) : p;
-  if constexpr (MINMAX) {
-    p = (lane & ~1) == 10 ? (const uint32_t*)(st.mn + s) + (lane & 1) : p;
-    p = (lane & ~1) == 12 ? (const uint32_t*)(st.mx + s) + (lane & 1) : p;
-  }
-  return p;
-}
-
-__device__ __forceinline__ int64_t hdr_i64(uint32_t hw, int k) {
-  return (int64_t)(((uint64_t)__builtin_amdgcn_readlane(hw, k + 1) << 32) | (uint32_t)__builtin_amdgcn_readlane(hw, k));
-}
-
 __device__ __forceinline__ int64_t rfl64(int64_t v) {
   const int lo = __builtin_amdgcn_readfirstlane((int)(uint32_t)(uint64_t)v);
   const int hi = __builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)v >> 32));
@@ -1938,10 +1914,15 @@ struct SmallLDS {
   alignas(16) double mv[64 * VPL + 64 + 2];  // values grouped by gap, +inf after the last; [last] trash
   alignas(16) double tv[SMALL_TVN];        // entry values at pidx(i); +inf from E up to E+63 (<= 127)
   alignas(16) int2 tgd[SMALL_CAP + 2];     // entry (g, d) at i; [j0+2] read as successor; [129] trash
-  // per gap (padded index): first the member count (.x, the count atomics),
-  // then the record (m<<24 | k<<16 | member base<<8 | out base, G+d-1)
-  alignas(16) int2 gi[SMALL_TVN];
-  alignas(16) int32_t mi[64 * VPL + 2];    // exact rank pass: a member's insertion index; [last] trash
+  union {
+    // per gap (padded index): first the member count (.x, the count atomics),
+    // then the record (m<<24 | k<<16 | member base<<8 | out base, G+d-1)
+    alignas(16) int2 gi[SMALL_TVN];
+    // exact rank pass: a member's insertion index; [last] trash.  It shares
+    // the records' bytes: the values hold their records in registers by then,
+    // and the records are reset (zeroed) after the pass.
+    int32_t mi[64 * VPL + 2];
+  };
 #ifdef GK_LDS_PAD
   unsigned char pad[GK_LDS_PAD];  // occupancy experiments only
 #endif
@@ -1951,86 +1932,10 @@ struct SmallLDS {
 #endif
 };
 
-// A flush's values (the first p from the pending buffer pb, the rest from
-// xs; cnt <= 64*VPL) LDS-DMA'd into L.pbf (global_load_lds: wave-uniform LDS
-// base + size*lane, per-lane global address).  Returns the slot of value 0 in
-// L.pbf.  The caller waits vmcnt(0) before reading L.pbf and neither reads
-// nor refills it while the DMA is in flight.
-//  * p == 0 (one source): ONE 16-byte DMA -- lane c loads the c-th 16-byte
-//    chunk of the aligned window holding the values (value 0 lands in slot
-//    1 when xs is not 16-byte aligned); lanes past the window re-load its
-//    last chunk.  Every chunk loaded holds a needed value, so no byte
-//    outside the batch's pages is touched.
-//  * otherwise 4-byte DMAs: dword d = 64*i + lane (value d/2) at slot d/2.
-// The next flush's values (or the next stream's first flush's), LDS-DMA'd
-// from HBM while the current flush runs (no VGPRs held for them).  Its own
-// __shared__ object, not a SmallLDS member: the compiler then proves that the
-// flush's LDS accesses never alias a DMA in flight and adds no vmcnt waits
-// in front of them.
-template <int VPL>
-struct PrefetchLDS {
-  alignas(16) double pbf[64 * VPL + 64 * (VPL & 1)];  // (VPL 1: one 16-byte DMA fills 128 slots)
-};
-
-// LDS byte address of a __shared__ object (M0 operand of an LDS-DMA)
-__device__ __forceinline__ uint32_t gk_lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
-
-// One LDS-DMA wave instruction (global_load_lds_dword / _dwordx4): every
-// active lane loads SIZE bytes from its own global address into LDS at
-// lds + SIZE*lane.  Emitted as inline asm: the compiler's own LDS-DMA
-// tracking would put a vmcnt(0) in front of flush LDS accesses it cannot
-// prove disjoint from the buffer (measured: the tgd and gap-record accesses),
-// i.e. wait for the DMA mid-flush.  The compiler does not count this VMEM
-// operation; that only ever makes its own counted waits stronger (in-order
-// counter, the DMA is younger or older than whatever it waits for), never
-// weaker.  The reader of the buffer waits vmcnt(0) itself.
-template <int SIZE>
-__device__ __forceinline__ void gk_glds(const void* gsrc, uint32_t lds) {
-  uint32_t keep;
-  if constexpr (SIZE == 16)
-    __asm__ volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
-  else
-    __asm__ volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
-}
-
-template <int VPL>
-__device__ __forceinline__ int gk_dma_flush_values(PrefetchLDS<VPL>& L, const double* pb, int p, const double* xs,
-                                                   int cnt, int lane) {
-  if (cnt <= 0) return 0;
-  const uint32_t base = gk_lds_addr(&L.pbf[0]);
-  if (p == 0) {
-    const uintptr_t a = (uintptr_t)xs;
-    const int sh = (int)((a >> 3) & 1);
-    const int nch = (sh + cnt + 1) >> 1;
-    if (nch <= 32 * VPL) {
-      const char* a0 = (const char*)(a & ~(uintptr_t)15);
-#pragma unroll
-      for (int i = 0; i < VPL / 2 + (VPL & 1); ++i) {
-        if (64 * i >= nch) break;
-        const int c = min(64 * i + lane, nch - 1);
-        gk_glds<16>(a0 + 16 * c, base + 1024 * i);
-      }
-      return sh;
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < 2 * VPL; ++i) {
-    if (64 * i >= 2 * cnt) break;
-    const int d = 64 * i + lane;
-    const int ic = min(d >> 1, cnt - 1);
-    const double* src = ic < p ? pb + ic : xs + (ic - p);
-    gk_glds<4>((const char*)src + ((d & 1) << 2), base + 256 * i);
-  }
-  return 0;
-}
-
 // gap counters of the next flush (gi[].x, read and written only inside a
 // flush): padded indices 0 .. pidx(127) = 130 of the SMALL_TVN = 136 records
 static_assert(SMALL_CAP + (SMALL_CAP >> 5) + 4 == 136, "gi zeroing covers 136 records");
+static_assert(sizeof(int32_t) * (64 * 2 + 2) <= sizeof(int2) * 136, "mi fits in the records");
 // (The zero is made at each use: hoisted out of the stream loop, the compiler
 // keeps a 4-VGPR zero alive across the flush and, short of registers, spills
 // it -- its reload's vmcnt wait then stalls on the in-flight LDS-DMA.)
@@ -2092,22 +1997,20 @@ __device__ __forceinline__ int gi_m(int x) { return (int)((uint32_t)x >> 24); }
 // One value x of a gap (its record gi) at rank `rk` inside the gap: gk:93-99
 // for an entry's gap, gk:85-92 for the tail.  Both rules evaluated, one store:
 // an absorbed value (or an empty slot, !valid) goes to the trash slot.
-// Branch-free: the keep decision is integer arithmetic (no lane-mask logic
-// that the compiler would lower to exec-mask branches).  The tail's record
-// carries d = 0 in gi.y, so d is gi.y in both cases.
+// One value x of a gap (its record gi) at rank `rk` inside the gap: gk:93-99
+// for an entry's gap, gk:85-92 for the tail.  Both rules evaluated, one store:
+// an absorbed value (or an empty slot, !valid) goes to the trash slot.  (A
+// branch-free keep decision measured 14% slower on cfg3: the compiler's exec
+// branches skip the tail rule for most waves; profiles/r03f_ab_dma_emit_variants.txt.)
 template <int VPL>
 __device__ __forceinline__ void small_emit(SmallLDS<VPL>& L, bool in_gap, const CsDiv& cd, double x, int2 gi,
-                                           int rk, int vi) {  // vi = cnt-1-(value index): valid iff >= 0
+                                           int rk, bool valid) {
   const int k = gi_k(gi.x);
   const int q = cd.div(rk);
   const int rr = cd.rem(rk, q);
-  // gap: kept iff rk - k >= 0; tail: kept iff rr = cs-1 or rk = m-1 (both
-  // differences <= 0, so their max is 0 iff one of them is 0)
-  const int dg = rk - k;
-  const int dt = max(rr - (cd.cs - 1), rk - gi_m(gi.x) + 1);  // <= 0
-  const int pos = gi_ob(gi.x) + (in_gap ? dg : q);
-  const int drop = (in_gap ? dg : (dt >> 31)) | vi;  // < 0: not kept
-  small_put(L, drop < 0 ? GK_SMALL_TRASH : pos, x, in_gap ? 1 : rr + 1, gi.y);
+  const int pos = gi_ob(gi.x) + (in_gap ? rk - k : q);
+  const bool keep = valid && (in_gap ? rk >= k : (rr == cd.cs - 1 || rk == gi_m(gi.x) - 1));
+  small_put(L, keep ? pos : GK_SMALL_TRASH, x, in_gap ? 1 : rr + 1, in_gap ? gi.y : 0);
 }
 
 // ---- in-register sort of 128 doubles, two per lane ------------------------
@@ -2380,7 +2283,7 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
       const bool v = j0 + e < E;
       gk[e] = make_int2((em[e] << 24) | (ek[e] << 16) | (int)((base >> 8) & 0xff00u) | (int)(base & 0xffu),
                         eG[e] + ed[e] - 1);
-      small_put(L, (v & ekeep[e]) ? (int)(base & 0xffffu) + em[e] - ek[e] : GK_SMALL_TRASH, ev[e], eG[e], ed[e]);
+      small_put(L, (v && ekeep[e]) ? (int)(base & 0xffffu) + em[e] - ek[e] : GK_SMALL_TRASH, ev[e], eG[e], ed[e]);
       base += v ? (((uint32_t)em[e] << 16) | (uint32_t)(em[e] - ek[e] + (ekeep[e] ? 1 : 0))) : 0u;
     }
     L.gi[pj0] = gk[0];
@@ -2472,7 +2375,7 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
       }
     }
 #pragma unroll
-    for (int r = 0; r < VPL; ++r) small_emit(L, xb[r] < pE8, cd, xv[r], gv[r], rk[r], cnt - 1 - (lane + 64 * r));
+    for (int r = 0; r < VPL; ++r) small_emit(L, xb[r] < pE8, cd, xv[r], gv[r], rk[r], lane + 64 * r < cnt);
     GK_MARK(L, 5);
   } else {
     // A large gap (the first flush, where every value is tail, or an
@@ -2524,7 +2427,7 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
 #pragma unroll
     for (int r = 0; r < VPL; ++r) {
       const int2 gv = *(const int2*)((const char*)L.gi + xb[r]);
-      small_emit(L, xb[r] < pE8, cd, xv[r], gv, q[r] - gi_mb(gv.x), cnt - 1 - (lane + 64 * r));
+      small_emit(L, xb[r] < pE8, cd, xv[r], gv, q[r] - gi_mb(gv.x), lane + 64 * r < cnt);
     }
     GK_MARK(L, 6);
   }
@@ -2778,7 +2681,6 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
                                                      unsigned long long* __restrict__ work, int nstat,
                                                      int fs_pace, int fs_lag) {
   __shared__ __attribute__((aligned(16))) SmallLDS<VPL> L;
-  __shared__ __attribute__((aligned(16))) PrefetchLDS<VPL> PF;
   const int lane = threadIdx.x;
   const int P = st.P;
 #ifdef GK_PROF
@@ -2787,23 +2689,10 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
     L.prof_t = gk_cycles();
   }
 #endif
-  // Streams are handed out dynamically (one atomic per GK_WORK_CHUNK streams
-  // on `work`, zeroed before the launch), so waves on slower CUs simply take
-  // fewer streams.  Everything a stream needs from memory before its first
-  // flush is fetched during the previous stream's flushes, so that no HBM
-  // latency is exposed at a stream's start (round 2's section profile: ~10%
-  // of the launch at "loop top + a stream's first values"):
-  //   flush 1 of stream s: the hand-out atomic for the next stream (wn);
-  //   flush 2: wn's header (one lane-distributed VGPR load, `hw`);
-  //   flush 3: the header is taken into `hn` (landed by then);
-  //   last flush: wn's first flush values, LDS-DMA'd into L.pbf.
-  // Inside a stream, each flush LDS-DMAs the next flush's values into L.pbf
-  // at its start (they land while it runs).  A stream with fewer flushes
-  // fetches what is missing at its end (the latency is then exposed, as
-  // before).  Waits: an explicit vmcnt(0) before L.pbf is read (at a flush's
-  // top, after the previous flush's work); the compiler's own waits on the
-  // atomic / header results are placed before any DMA is issued in that
-  // flush, so they never wait on one.
+  // Streams are handed out dynamically (one atomic per stream on `work`,
+  // zeroed before the launch), so waves on slower CUs simply take fewer
+  // streams; the next stream's id and header are fetched one stream ahead.
+  GKHdrV hv;
 #ifndef GK_WORK_PARTS
 #define GK_WORK_PARTS 8  // counters (one 128-B line each); a wave uses blockIdx % parts
 #endif
@@ -2817,83 +2706,38 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
   // the query's q values, the same for every stream: lane l holds q l
   const double qpre = (qs && lane < nq) ? qs[lane] : 0.0;
   int64_t cur = 0, cend = 0;
-  unsigned long long gv = 0;
-  bool gpend = false;  // a hand-out atomic is in flight (its result in gv, lane 0)
-  auto grab_issue = [&]() {
-    if (cur >= cend && !gpend) {
-      gv = 0;
-      if (lane == 0) gv = atomicAdd(work + 16 * part, (unsigned long long)GK_WORK_CHUNK);
-      gpend = true;
-    }
-  };
-  auto grab_take = [&]() -> int64_t {
+  auto grab = [&]() -> int64_t {
     if (cur >= cend) {
-      grab_issue();
-      cur = pbeg + rfl64((int64_t)gv);
-      gpend = false;
+      unsigned long long v = 0;
+      if (lane == 0) v = atomicAdd(work + 16 * part, (unsigned long long)GK_WORK_CHUNK);
+      cur = pbeg + rfl64((int64_t)v);
       cend = min(cur + GK_WORK_CHUNK, pend);
       if (cur >= pend) return count;
     }
     return cur++;
   };
-  // stream header, one 32-bit word per lane (hdr_lane_ptr): loaded into hw,
-  // copied into hn once landed (the copy is what waits), read with readlane
-  uint32_t hw = 0, hn = 0;
-  auto hdr_issue = [&](int64_t s) { hw = *hdr_lane_ptr<!FS>(st, offs, s, lane); };
-  int64_t w = grab_take();
-  if (w < count) {
-    hdr_issue(w);
-    hn = hw;
-  }
-  int64_t pf_s = -1;  // the stream whose first flush values L.pbf holds
-  int pfsh = 0;       // slot of the first value in L.pbf
+  int64_t w = grab();
+  if (w < count) gk_hdr_issue<!FS>(hv, st, offs, w);
   for (; w < count;) {
     const int64_t s = w;
-    const int32_t scls = (int32_t)__builtin_amdgcn_readlane(hn, 0);
-    const int32_t sslot = (int32_t)__builtin_amdgcn_readlane(hn, 1);
-    int p = (int)__builtin_amdgcn_readlane(hn, 2);
-    int E = (int)__builtin_amdgcn_readlane(hn, 3);
-    int64_t n = hdr_i64(hn, 4);
-    const int64_t xo = hdr_i64(hn, 6);
-    const int64_t xe = hdr_i64(hn, 8);
+    const int64_t wn = grab();
+    const int32_t scls = __builtin_amdgcn_readfirstlane(hv.cls);
+    const int32_t sslot = __builtin_amdgcn_readfirstlane(hv.slot);
+    int p = __builtin_amdgcn_readfirstlane(hv.pend);
+    int E = __builtin_amdgcn_readfirstlane(hv.E);
+    int64_t n = rfl64(hv.n);
+    const int64_t xo = rfl64(hv.xo);
+    const int64_t xe = rfl64(hv.xe);
     // with the stats role in this launch, _min/_max are not final yet: markers
-    const double smn = FS ? __longlong_as_double(GK_QMARK_MIN) : __longlong_as_double(hdr_i64(hn, 10));
-    const double smx = FS ? __longlong_as_double(GK_QMARK_MAX) : __longlong_as_double(hdr_i64(hn, 12));
-    const bool have_pf = pf_s == s;
-    pf_s = -1;
-    // the next stream, fetched in stages (see above); nst: 0 nothing, 1 atomic
-    // issued, 2 header issued (wn known), 3 header in hn
-    int nst = 0;
-    int64_t wn = count;
-    auto next_step = [&]() {
-      if (nst == 0) {
-        grab_issue();
-        nst = 1;
-      } else if (nst == 1) {
-        wn = grab_take();
-        if (wn < count) hdr_issue(wn);
-        nst = 2;
-      } else if (nst == 2) {
-        hn = hw;
-        nst = 3;
-      }
-    };
-    auto next_finish = [&]() {
-      while (nst < 3) next_step();
-    };
-    if (scls != 0) {  // promoted: handled by its class launch
-      next_finish();
-      w = wn;
-      continue;
-    }
+    const double smn = FS ? __longlong_as_double(GK_QMARK_MIN) : __longlong_as_double(rfl64(__double_as_longlong(hv.mn)));
+    const double smx = FS ? __longlong_as_double(GK_QMARK_MAX) : __longlong_as_double(rfl64(__double_as_longlong(hv.mx)));
+    if (wn < count) gk_hdr_issue<!FS>(hv, st, offs, wn);
+    w = wn;
+    if (scls != 0) continue;  // promoted: handled by its class launch
     const int64_t Lx = xe - xo;
     // force 1: flush only if values are pending (size/quantile, gk:45, 166, 197)
     // force 2: unconditional merge_compress() (merge, gk:122, 126, 137)
-    if (Lx <= 0 && !((force == 1 && p > 0) || (force == 2 && n > 0)) && !qs) {
-      next_finish();
-      w = wn;
-      continue;
-    }
+    if (Lx <= 0 && !((force == 1 && p > 0) || (force == 2 && n > 0)) && !qs) continue;
     GKRec* __restrict__ tab = gk_table_ptr_cs(st, s, scls, sslot);
     double* __restrict__ pb = st.pbuf + s * (int64_t)st.pmax;
     // an imported / merged table without room for the padding, or a stream
@@ -2942,52 +2786,30 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
         if (!((force == 1 && p + nadd > 0) || force == 2)) break;
       }
       const int cnt = p + (int)nadd;
-#ifdef GK_NO_DMA
-      if (false) {
-#else
-      if (flushed || have_pf) {
-#endif
-        // DMA'd during the previous flush (or the previous stream's last)
-        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-        for (int r = 0; r < VPL; ++r) xv[r] = (lane + 64 * r < cnt) ? PF.pbf[pfsh + lane + 64 * r] : 0.0;
-        __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read before the buffer is refilled
-      } else {
-        gk_load_flush_values<VPL>(xv, pb, p, x ? x + xo + used : pb, cnt, lane);
-      }
-#ifdef GK_NO_DMA
-      if (false)
-#endif
-      next_step();  // (before any DMA of this flush: its waits are on older loads only)
+      if (!flushed) gk_load_flush_values<VPL>(xv, pb, p, x ? x + xo + used : pb, cnt, lane);
       const int64_t nused = used + nadd;
-      // the next flush's values: this stream's (if it flushes again: full
-      // period, or a requested flush of the leftover), else the next stream's
-      // first flush's
-      const int64_t rest = autof ? Lx - nused : 0;
-#ifdef GK_NO_DMA
-      if (false) {
-      } else if (false) {
-#else
-      if (rest > 0 && (rest >= P || force != 0)) {
-#endif
-        pfsh = gk_dma_flush_values<VPL>(PF, pb, 0, x + xo + nused, (int)min((int64_t)P, rest), lane);
-      } else if (nst == 3 && wn < count && (int32_t)__builtin_amdgcn_readlane(hn, 0) == 0) {
-        const int np = (int)__builtin_amdgcn_readlane(hn, 2);
-        const int64_t nLx = hdr_i64(hn, 8) - hdr_i64(hn, 6);
-        const int nc = (int)min((int64_t)np + (nLx > 0 ? nLx : 0), (int64_t)P);
-        pfsh = gk_dma_flush_values<VPL>(PF, st.pbuf + wn * (int64_t)st.pmax, np, x + hdr_i64(hn, 6), nc, lane);
-        pf_s = wn;
-      }
+      // the next flush's values (or the leftover tail), loaded one flush ahead
+      const int navail = autof ? (int)min((int64_t)P, Lx - nused) : 0;
+      double xn[VPL];
+#pragma unroll
+      for (int r = 0; r < VPL; ++r) xn[r] = 0.0;
+      auto prefetch = [&]() {
+        if (navail > 0) {
+          const double* base = x + xo + nused;
+#pragma unroll
+          for (int r = 0; r < VPL; ++r) xn[r] = base[min(lane + 64 * r, navail - 1)];
+        }
+      };
       n += nadd;
       nm1 += (double)(int)nadd;
       const int T = __builtin_amdgcn_readfirstlane((int)(st.two_eps * nm1));
       GK_MARK(L, 8);
       int nE;
       if constexpr (SMALL_CAP > 128)
-        nE = E <= 127 ? flush_small<VPL, 2>(L, E, xv, cnt, T, lane, [] {})
-                      : flush_small<VPL, 4>(L, E, xv, cnt, T, lane, [] {});
+        nE = E <= 127 ? flush_small<VPL, 2>(L, E, xv, cnt, T, lane, prefetch)
+                      : flush_small<VPL, 4>(L, E, xv, cnt, T, lane, prefetch);
       else
-        nE = flush_small<VPL, 2>(L, E, xv, cnt, T, lane, [] {});
+        nE = flush_small<VPL, 2>(L, E, xv, cnt, T, lane, prefetch);
       if (nE < 0) {
         ok = false;
         break;
@@ -2997,18 +2819,23 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
       p = 0;
       need = P;
       flushed = true;
-      GK_MARK(L, 10);
+#pragma unroll
+      for (int r = 0; r < VPL; ++r) xv[r] = (lane + 64 * r < navail) ? xn[r] : 0.0;
+      GK_MARK(L, 10);  // (profiling builds: the wait for the prefetched values)
       if (!autof) {
         final_done = true;
         break;
       }
     }
-    next_finish();
     if (ok && !final_done) {
-      // values left after the last flush (fewer than need, no flush
-      // requested): they stay pending
-      const int64_t rem = Lx - used;
-      for (int64_t i = lane; i < rem; i += 64) pb[p + i] = x[xo + used + i];
+      const int64_t rem = Lx - used;  // < need: stays pending
+      if (flushed) {
+#pragma unroll
+        for (int r = 0; r < VPL; ++r)
+          if (lane + 64 * r < rem) pb[lane + 64 * r] = xv[r];
+      } else {
+        for (int64_t i = lane; i < rem; i += 64) pb[p + i] = x[xo + used + i];
+      }
       p += (int)rem;
       n += rem;
     }
@@ -3020,7 +2847,6 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
         ovf_list[k] = (int32_t)s;
       }
       wsync<false>();
-      w = wn;
       continue;
     }
     if (qs) {
@@ -3050,7 +2876,6 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
     }
     wsync<false>();
     GK_MARK(L, 9);
-    w = wn;
   }
 #ifdef GK_PROF
   if (lane == 0)
