@@ -249,6 +249,33 @@ __device__ __forceinline__ void gk_hdr_issue(GKHdrV& h, const GKState& st, const
   }
 }
 
+// The same header spread over the lanes of ONE register (lane k loads word
+// k: 0 cls, 1 slot, 2 pend, 3 E, 4-5 n, 6-7 xo, 8-9 xe, 10-11 mn, 12-13 mx)
+// for k_ingest_small, where the prefetch stays live across the whole stream:
+// one VGPR instead of 10-14.  Read back with gk_hdr1_word/_dword.
+template <bool MINMAX>
+__device__ __forceinline__ uint32_t gk_hdr1_issue(const GKState& st, const int64_t* offs, int64_t s, int lane) {
+  constexpr int NW = MINMAX ? 14 : 10;
+  const uint32_t* p = (const uint32_t*)(st.cls + s);
+  if (lane == 1) p = (const uint32_t*)(st.slot + s);
+  if (lane == 2) p = (const uint32_t*)(st.pend + s);
+  if (lane == 3) p = (const uint32_t*)(st.E + s);
+  if (lane >= 4) p = (const uint32_t*)(st.n + s) + (lane - 4);
+  if (lane >= 6) p = (const uint32_t*)(offs + s) + (lane - 6);  // xo, then xe (offs[s + 1])
+  if constexpr (MINMAX) {
+    if (lane >= 10) p = (const uint32_t*)(st.mn + s) + (lane - 10);
+    if (lane >= 12) p = (const uint32_t*)(st.mx + s) + (lane - 12);
+  }
+  uint32_t w = 0;
+  if (lane < NW) w = *p;
+  return w;
+}
+__device__ __forceinline__ int32_t gk_hdr1_word(uint32_t w, int k) { return __builtin_amdgcn_readlane((int)w, k); }
+__device__ __forceinline__ int64_t gk_hdr1_dword(uint32_t w, int k) {
+  return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)w, k + 1) << 32) |
+                   (uint32_t)__builtin_amdgcn_readlane((int)w, k));
+}
+
 __device__ __forceinline__ int64_t rfl64(int64_t v) {
   const int lo = __builtin_amdgcn_readfirstlane((int)(uint32_t)(uint64_t)v);
   const int hi = __builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)v >> 32));
@@ -1905,6 +1932,10 @@ __device__ __forceinline__ int pidx(int i) { return i + (i >> 5); }
 // a lane with nothing to store writes to a slot nobody reads (GK_SMALL_TRASH
 // in tv/tgd, the lane's own word past the counts, the last mv slot), which
 // spares the exec-mask save / restore / branch of every divergent store.
+// (One shared slot is right: stores of one address from several lanes of a
+// group merge, while a slot per lane -- tried, GK_TRASH_LANES in round 3 --
+// lands on the live stores' banks: +14% bank-conflict cycles, no gain;
+// profiles/r03q_trash_slots_ab.txt.)
 #define GK_SMALL_TRASH (SMALL_CAP + 1)  // logical slot: tv[pidx(129)], tgd[129]
 static_assert(SMALL_CAP == 128, "k_ingest_small is laid out for the 128-entry class (K = 2 entries per lane)");
 template <int VPL>
@@ -2083,6 +2114,9 @@ template <int VPL, int K, typename AfterSearch>
 __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const double (&xv)[VPL], const int cnt,
                                            const int T, const int lane, AfterSearch&& after_search) {
   static_assert(K == 2, "the 128-entry class holds 2 entries per lane");
+  // the chunk-size divider first: its magic-number load (a scalar load)
+  // returns during the gap search instead of stalling after the scan
+  const CsDiv cd = make_csdiv(T);
   if constexpr (VPL == 2) {
     // ---- empty table (every stream's first flush): all values are tail
     //      (gk:85-92), so the flush is a sort and a cut into chunks of
@@ -2098,7 +2132,6 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
       }
       if (!(__builtin_amdgcn_ballot_w64(pz) != 0 && __builtin_amdgcn_ballot_w64(nz) != 0)) {
         after_search();
-        const CsDiv cd = make_csdiv(T);
         const int newE = cd.cs > 128 ? (cnt > 0 ? 1 : 0) : cd.div(cnt + cd.cs - 1);
         if (newE > SMALL_CAP - 1) return -1;
         double a[2];
@@ -2251,7 +2284,6 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
       c = ekeep[e] ? 0 : eG[e];
     }
   }
-  const CsDiv cd = make_csdiv(T);
   uint32_t sm = 0, so = 0;
 #pragma unroll
   for (int e = 0; e < K; ++e) {
@@ -2692,7 +2724,7 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
   // Streams are handed out dynamically (one atomic per stream on `work`,
   // zeroed before the launch), so waves on slower CUs simply take fewer
   // streams; the next stream's id and header are fetched one stream ahead.
-  GKHdrV hv;
+  uint32_t hv = 0;  // the next stream's header, one word per lane (gk_hdr1_issue)
 #ifndef GK_WORK_PARTS
 #define GK_WORK_PARTS 8  // counters (one 128-B line each); a wave uses blockIdx % parts
 #endif
@@ -2717,21 +2749,21 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
     return cur++;
   };
   int64_t w = grab();
-  if (w < count) gk_hdr_issue<!FS>(hv, st, offs, w);
+  if (w < count) hv = gk_hdr1_issue<!FS>(st, offs, w, lane);
   for (; w < count;) {
     const int64_t s = w;
     const int64_t wn = grab();
-    const int32_t scls = __builtin_amdgcn_readfirstlane(hv.cls);
-    const int32_t sslot = __builtin_amdgcn_readfirstlane(hv.slot);
-    int p = __builtin_amdgcn_readfirstlane(hv.pend);
-    int E = __builtin_amdgcn_readfirstlane(hv.E);
-    int64_t n = rfl64(hv.n);
-    const int64_t xo = rfl64(hv.xo);
-    const int64_t xe = rfl64(hv.xe);
+    const int32_t scls = gk_hdr1_word(hv, 0);
+    const int32_t sslot = gk_hdr1_word(hv, 1);
+    int p = gk_hdr1_word(hv, 2);
+    int E = gk_hdr1_word(hv, 3);
+    int64_t n = gk_hdr1_dword(hv, 4);
+    const int64_t xo = gk_hdr1_dword(hv, 6);
+    const int64_t xe = gk_hdr1_dword(hv, 8);
     // with the stats role in this launch, _min/_max are not final yet: markers
-    const double smn = FS ? __longlong_as_double(GK_QMARK_MIN) : __longlong_as_double(rfl64(__double_as_longlong(hv.mn)));
-    const double smx = FS ? __longlong_as_double(GK_QMARK_MAX) : __longlong_as_double(rfl64(__double_as_longlong(hv.mx)));
-    if (wn < count) gk_hdr_issue<!FS>(hv, st, offs, wn);
+    const double smn = __longlong_as_double(FS ? GK_QMARK_MIN : gk_hdr1_dword(hv, 10));
+    const double smx = __longlong_as_double(FS ? GK_QMARK_MAX : gk_hdr1_dword(hv, 12));
+    if (wn < count) hv = gk_hdr1_issue<!FS>(st, offs, wn, lane);
     w = wn;
     if (scls != 0) continue;  // promoted: handled by its class launch
     const int64_t Lx = xe - xo;
