@@ -23,6 +23,8 @@
 #include <limits>
 #include <string>
 #include <thread>
+
+#include "gk_host_stats.h"
 #include <vector>
 
 #include "gk_cpu.h"
@@ -121,13 +123,7 @@ int64_t threshold(const gk_set* h, int64_t n) {
 }
 
 // gk:52-59 for one value
-inline void add_stats(Stream& s, double v) {
-  s.n += 1;
-  s.sum += v;
-  s.avg += (v - s.avg) * (1.0 / (double)s.n);
-  if (v < s.mn) s.mn = v;
-  if (v > s.mx) s.mx = v;
-}
+inline void add_stats(Stream& s, double v) { gk_host_stat_step(s.n, s.sum, s.avg, s.mn, s.mx, v); }
 
 // Stable order of the pending values by value (gk:71-72: Python's sorted();
 // -0.0 == +0.0, so equal keys keep insertion order): sorted by (value,

@@ -6,13 +6,18 @@
 // declared in include/gk_capi.h with the reference method it replaces.
 #include <hip/hip_runtime.h>
 
+#include <sched.h>
+
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "gk_capi.h"
@@ -20,6 +25,7 @@
 #include "gk_format.h"
 #include "gk_launch.h"
 #include "gk_state.h"
+#include "gk_host_stats.h"
 
 namespace {
 
@@ -127,6 +133,34 @@ struct gk_set {
   int fused_stats = 7;
   // gk_fold_packed: receives the packed states merged into this set (made on first use)
   gk_set* fold_scratch = nullptr;
+  // Host-walked chains: the gk:52-59 chains of the
+  // longest streams run on host cores beside the GPU ingest.  hc_min: shortest
+  // stream taken (0: off; GK_HOST_CHAINS=0 / GK_HOST_CHAIN_MIN); hc_threads:
+  // host threads (GK_HOST_CHAIN_THREADS); at most 4 x hc_threads x the
+  // longest length values go to the host per call.
+  int64_t hc_min = 0;
+  int hc_rel = 75;  // ... and >= this % of the longest stream (GK_HOST_CHAIN_REL)
+  int hc_threads = 1;
+  GKHostChainRec* d_hc = nullptr;   // GK_HC_MAX records (device)
+  int32_t* d_hc_count = nullptr;
+  GKHostChainRec* h_hc = nullptr;   // pinned copies
+  int32_t* h_hc_count = nullptr;
+  hipEvent_t ev_hc = nullptr;       // the records' D2H copy
+  bool hc_active = false;           // this call enqueued k_hc_prep
+  const double* hc_x = nullptr;     // the call's values
+  // one copy stream for every host thread's chunk copies, made right after
+  // `aux` so that it gets a hardware queue of its own (the box runs 4 per
+  // process: a copy stream sharing the ingest's or aux's queue waits behind
+  // their kernels -- 16 per-thread streams gave 12 GB/s instead of ~55);
+  // per host thread two pinned chunk buffers and their events
+  hipStream_t hc_copy = nullptr;
+  // k_presort of the long streams' flush batches runs here beside the short
+  // streams' chains (k_stats on the caller's stream); the ingest waits for it
+  hipStream_t aux2 = nullptr;
+  hipEvent_t ev_presort = nullptr;
+  std::vector<hipStream_t> hc_streams;
+  std::vector<double*> hc_buf;
+  std::vector<hipEvent_t> hc_ev;
   // timing: event pairs recorded around the timed launches, summed at read
   bool timing = false;
   std::vector<hipEvent_t> tev_flush, tev_stats;
@@ -348,6 +382,7 @@ int grow_pools(gk_set* h, hipStream_t s) {
     const int64_t cap = std::max<int64_t>(need + need / 8, 1 << 20);
     HIP_TRY(hipStreamSynchronize(s));
     HIP_TRY(hipStreamSynchronize(h->aux));
+    HIP_TRY(hipStreamSynchronize(h->aux2));
     if (h->ps.ws) (void)hipFree(h->ps.ws);
     h->ps.ws = nullptr;
     h->ps.ws_cap = 0;
@@ -435,6 +470,121 @@ hipError_t launch_class(gk_set* h, int c, const double* x, const int64_t* offs, 
 // only lists the long streams)
 bool stats_fused(const gk_set* h) { return h->fused_stats > 0 && h->st.cap[0] == GK_SMALL_CAP; }
 
+// doubles per pinned chunk copy (GK_HOST_CHAIN_CHUNK_MB, default 8 MiB)
+const int64_t kHcChunk = []() {
+  int64_t mb = 8;
+  if (const char* e = getenv("GK_HOST_CHAIN_CHUNK_MB")) mb = std::max<int64_t>(1, std::min<int64_t>(256, atoll(e)));
+  return mb << 17;
+}();
+
+// Per-thread copy stream, chunk buffers and events for the first `t` host
+// threads (made on first use, kept until gk_destroy).
+int hc_ensure(gk_set* h, int t) {
+  while ((int)h->hc_streams.size() < t) {
+    h->hc_streams.push_back(h->hc_copy);
+    for (int b = 0; b < 2; ++b) {
+      double* p = nullptr;
+      if (hipHostMalloc(&p, kHcChunk * sizeof(double)) != hipSuccess) return fail(GK_E_NOMEM, "host-chain buffer");
+      h->hc_buf.push_back(p);
+      hipEvent_t e = nullptr;
+      HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      h->hc_ev.push_back(e);
+    }
+  }
+  return GK_OK;
+}
+
+// Walk the chains k_hc_prep picked (blocking): the longest streams first,
+// each on one host thread, its values streamed device -> pinned host in
+// 2 MiB chunks (the next chunk's copy in flight while the chain walks this
+// one) and fed to the host engine's gk:52-59 step.  The final state goes
+// back into the pinned records (applied on the device by stats_join).
+int run_host_chains(gk_set* h, int* taken) {
+  *taken = 0;
+  HIP_TRY(hipEventSynchronize(h->ev_hc));
+  const int K = std::min(*h->h_hc_count, GK_HC_MAX);
+  if (K <= 0) return GK_OK;
+  const int T = std::max(1, std::min(h->hc_threads, K));
+  int rc = hc_ensure(h, T);
+  if (rc) return rc;
+  std::atomic<int> next{0};
+  std::atomic<int> err{0};
+  std::vector<std::string> msg(T);
+  std::vector<double> t_walk(T, 0.0), t_wait(T, 0.0);
+  std::vector<int64_t> v_done(T, 0);
+  using clk = std::chrono::steady_clock;
+  const auto t_start = clk::now();
+  auto sec = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double>(b - a).count(); };
+  auto worker = [&](int t) {
+    hipStream_t hs = h->hc_streams[t];
+    double* buf[2] = {h->hc_buf[2 * t], h->hc_buf[2 * t + 1]};
+    hipEvent_t ev[2] = {h->hc_ev[2 * t], h->hc_ev[2 * t + 1]};
+    for (;;) {
+      const int k = next.fetch_add(1);
+      if (k >= K || err.load()) return;
+      GKHostChainRec& r = h->h_hc[k];
+      GKHostStats hs_state{r.n, r.sum, r.avg, r.mn, r.mx};
+      const double* src = h->hc_x + r.xo;
+      auto issue = [&](int64_t off, int b) -> bool {
+        const int64_t c = std::min(kHcChunk, r.len - off);
+        return hipMemcpyAsync(buf[b], src + off, c * sizeof(double), hipMemcpyDefault, hs) == hipSuccess &&
+               hipEventRecord(ev[b], hs) == hipSuccess;
+      };
+      bool ok = r.len <= 0 || issue(0, 0);
+      int cur = 0;
+      for (int64_t off = 0; ok && off < r.len;) {
+        const int64_t c = std::min(kHcChunk, r.len - off);
+        if (off + c < r.len) ok = issue(off + c, cur ^ 1);
+        const auto a = clk::now();
+        ok = ok && hipEventSynchronize(ev[cur]) == hipSuccess;
+        if (!ok) break;
+        const auto b = clk::now();
+        gk_host_stat_run(hs_state, buf[cur], c);
+        t_wait[t] += sec(a, b);
+        t_walk[t] += sec(b, clk::now());
+        v_done[t] += c;
+        off += c;
+        cur ^= 1;
+      }
+      if (!ok) {
+        msg[t] = hipGetErrorString(hipGetLastError());
+        err.store(1);
+        (void)hipStreamSynchronize(hs);
+        return;
+      }
+      r.sum = hs_state.sum;
+      r.avg = hs_state.avg;
+      r.mn = hs_state.mn;
+      r.mx = hs_state.mx;
+    }
+  };
+  std::vector<std::thread> pool;
+  pool.reserve(T - 1);
+  for (int t = 1; t < T; ++t) pool.emplace_back(worker, t);
+  worker(0);
+  for (auto& th : pool) th.join();
+  static const bool hc_trace = getenv("GK_HC_TRACE") != nullptr;
+  if (hc_trace) {
+    double w = 0, q = 0;
+    int64_t v = 0;
+    for (int t = 0; t < T; ++t) {
+      w += t_walk[t];
+      q += t_wait[t];
+      v += v_done[t];
+    }
+    fprintf(stderr, "[gk] host chains: %d streams, %lld values on %d threads in %.1f ms (walk %.1f ms = %.2f ns/value, "
+            "copy waits %.1f ms, summed over threads)\n", K, (long long)v, T, 1e3 * sec(t_start, clk::now()), 1e3 * w,
+            v ? 1e9 * w / (double)v : 0.0, 1e3 * q);
+  }
+  if (err.load()) {
+    for (const std::string& m : msg)
+      if (!m.empty()) return fail(GK_E_HIP, "host-walked chains: chunk copy failed: %s", m.c_str());
+    return fail(GK_E_HIP, "host-walked chains: chunk copy failed");
+  }
+  *taken = K;
+  return GK_OK;
+}
+
 int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s) {
   hipEvent_t t0 = h->timing ? timing_event(h->tev_stats, h->n_stats) : nullptr;
   if (t0) HIP_TRY(hipEventRecord(t0, s));
@@ -446,10 +596,29 @@ int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s) {
   HIP_TRY(gk_launch_stats(h->st, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->ps, s));
   HIP_TRY(hipEventRecord(h->ev_fork, s));
   HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_fork, 0));
-  HIP_TRY(gk_launch_stats_long(h->st, x, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->aux));
+  // the longest chains to host cores (k_hc_prep picks them; k_stats_long
+  // skips them); the host walks them in stats_join, while the GPU ingests
+  h->hc_active = false;
+  if (h->hc_min > 0) {
+    HIP_TRY(gk_launch_hc_prep(h->st, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->hc_min, h->hc_rel,
+                              4 * (int64_t)h->hc_threads, h->d_hc, h->d_hc_count, h->aux));
+    HIP_TRY(hipMemcpyAsync(h->h_hc_count, h->d_hc_count, sizeof(int32_t), hipMemcpyDeviceToHost, h->aux));
+    HIP_TRY(hipMemcpyAsync(h->h_hc, h->d_hc, GK_HC_MAX * sizeof(GKHostChainRec), hipMemcpyDeviceToHost, h->aux));
+    HIP_TRY(hipEventRecord(h->ev_hc, h->aux));
+    h->hc_x = x;
+  }
+  HIP_TRY(gk_launch_stats_long(h->st, x, offs, h->d_long_list, h->d_long_n, h->d_long_count,
+                               h->hc_min > 0 ? h->d_hc_count : nullptr, h->aux));
+  h->hc_active = h->hc_min > 0;  // (stats_join walks the picked chains)
   HIP_TRY(hipEventRecord(h->ev_join, h->aux));
+  const bool presort = h->ps.list_ws && h->ps.ws && h->ps.ws_cap > 0;
+  if (presort) {
+    HIP_TRY(hipStreamWaitEvent(h->aux2, h->ev_fork, 0));
+    HIP_TRY(gk_launch_presort(h->st, x, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->ps, h->aux2));
+    HIP_TRY(hipEventRecord(h->ev_presort, h->aux2));
+  }
   if (!stats_fused(h)) HIP_TRY(gk_launch_stats_short(h->st, x, offs, s));
-  HIP_TRY(gk_launch_presort(h->st, x, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->ps, s));
+  if (presort) HIP_TRY(hipStreamWaitEvent(s, h->ev_presort, 0));
   if (h->ps.ws_need) HIP_TRY(hipMemcpyAsync(h->h_ws_need, h->ps.ws_need, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   hipEvent_t t1 = h->timing ? timing_event(h->tev_stats, h->n_stats) : nullptr;
   if (t1) HIP_TRY(hipEventRecord(t1, s));
@@ -457,9 +626,20 @@ int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s) {
 }
 
 int stats_join(gk_set* h, hipStream_t s, const GKQuery& q) {
+  int rc = GK_OK, taken = 0;
+  if (h->hc_active) {
+    h->hc_active = false;
+    rc = run_host_chains(h, &taken);  // blocks this thread while the GPU ingests
+  }
   HIP_TRY(hipStreamWaitEvent(s, h->ev_join, 0));
+  if (taken > 0) {
+    // (the next call's record readback is ordered after this copy: its fork
+    // waits on `s`)
+    HIP_TRY(hipMemcpyAsync(h->d_hc, h->h_hc, taken * sizeof(GKHostChainRec), hipMemcpyHostToDevice, s));
+    HIP_TRY(gk_launch_hc_apply(h->st, h->d_hc, h->d_hc_count, s));
+  }
   HIP_TRY(gk_launch_query_list(h->st, h->d_long_list, h->d_long_count, q, s));
-  return GK_OK;
+  return rc;
 }
 
 // The ingest / flush launches of one call, with no host round trip: class 0
@@ -612,6 +792,24 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
   h->device = device;
   h->vpl = h->P <= 1024 ? vpl_for(h->P) : 0;  // (registers of the capacity-class kernels)
   if (const char* fs = getenv("GK_FUSED_STATS")) h->fused_stats = std::max(0, std::min(64, atoi(fs)));
+  // host-walked chains: streams of >= 2^20 values (GK_HOST_CHAIN_MIN; 0 or
+  // GK_HOST_CHAINS=0: off) on up to 16 host threads (GK_HOST_CHAIN_THREADS;
+  // the process's CPU share: its affinity set, OMP_NUM_THREADS if lower)
+  h->hc_min = (int64_t)1 << 20;
+  if (const char* e = getenv("GK_HOST_CHAIN_MIN")) h->hc_min = std::max<int64_t>(0, atoll(e));
+  if (const char* e = getenv("GK_HOST_CHAINS"))
+    if (atoi(e) == 0) h->hc_min = 0;
+  if (const char* e = getenv("GK_HOST_CHAIN_REL")) h->hc_rel = std::max(0, std::min(100, atoi(e)));
+  {
+    int t = 16;
+    cpu_set_t cs;
+    if (sched_getaffinity(0, sizeof(cs), &cs) == 0 && CPU_COUNT(&cs) > 0) t = std::min(t, CPU_COUNT(&cs));
+    if (const char* e = getenv("OMP_NUM_THREADS"))
+      if (atoi(e) > 0) t = std::min(t, atoi(e));
+    if (const char* e = getenv("GK_HOST_CHAIN_THREADS"))
+      if (atoi(e) > 0) t = atoi(e);
+    h->hc_threads = std::max(1, std::min(t, GK_HC_MAX));
+  }
   GKState& st = h->st;
   st.S = num_streams;
   st.eps = eps;
@@ -693,8 +891,16 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
   okm &= hipMalloc(&h->d_long_n, S * sizeof(int64_t)) == hipSuccess;
 
   okm &= hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking) == hipSuccess;
+  okm &= hipStreamCreateWithFlags(&h->hc_copy, hipStreamNonBlocking) == hipSuccess;
+  okm &= hipStreamCreateWithFlags(&h->aux2, hipStreamNonBlocking) == hipSuccess;
+  okm &= hipEventCreateWithFlags(&h->ev_presort, hipEventDisableTiming) == hipSuccess;
   okm &= hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) == hipSuccess;
   okm &= hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) == hipSuccess;
+  okm &= hipMalloc(&h->d_hc, GK_HC_MAX * sizeof(GKHostChainRec)) == hipSuccess;
+  okm &= hipMalloc(&h->d_hc_count, sizeof(int32_t)) == hipSuccess;
+  okm &= hipHostMalloc(&h->h_hc, GK_HC_MAX * sizeof(GKHostChainRec)) == hipSuccess;
+  okm &= hipHostMalloc(&h->h_hc_count, sizeof(int32_t)) == hipSuccess;
+  okm &= hipEventCreateWithFlags(&h->ev_hc, hipEventDisableTiming) == hipSuccess;
   if (h->P > 128 && !h->big[0]) {  // class 0 is a capacity-class kernel: presort long streams' batches
     okm &= hipMalloc(&h->ps.list_ws, S * sizeof(int64_t)) == hipSuccess;
     okm &= hipMalloc(&h->ps.list_b0, (S + 1) * sizeof(int64_t)) == hipSuccess;
@@ -734,7 +940,7 @@ int gk_destroy(gk_set* h) {
                   st.avg,     st.cls,        st.slot,        st.pbuf,        h->d_qs,
                   h->d_ctr,   h->d_zero_offs, h->d_long_list, h->d_long_n,
                   h->ps.list_ws, h->ps.list_b0, h->ps.ws,    h->ps.ws_need,  st.rtab,        st.n0,
-                  h->d_defer};
+                  h->d_defer, h->d_hc,       h->d_hc_count};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (int c = 0; c < GK_MAX_CLASSES; ++c)
@@ -744,10 +950,16 @@ int gk_destroy(gk_set* h) {
     if (h->d_ovfl[r]) (void)hipFree(h->d_ovfl[r]);
   for (auto* v : {&h->tev_flush, &h->tev_stats})
     for (hipEvent_t e : *v) (void)hipEventDestroy(e);
-  for (hipEvent_t e : {h->ev_fork, h->ev_join, h->ev_done, h->ev_qs})
+  for (hipEvent_t e : {h->ev_fork, h->ev_join, h->ev_done, h->ev_qs, h->ev_hc})
     if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : h->hc_ev) (void)hipEventDestroy(e);
+  if (h->hc_copy) (void)hipStreamDestroy(h->hc_copy);
+  if (h->aux2) (void)hipStreamDestroy(h->aux2);
+  if (h->ev_presort) (void)hipEventDestroy(h->ev_presort);
+  for (double* p : h->hc_buf) (void)hipHostFree(p);
   if (h->aux) (void)hipStreamDestroy(h->aux);
-  for (void* p : {(void*)h->h_ws_need, (void*)h->h_ovf, (void*)h->h_ctr, (void*)h->h_qs})
+  for (void* p : {(void*)h->h_ws_need, (void*)h->h_ovf, (void*)h->h_ctr, (void*)h->h_qs, (void*)h->h_hc,
+                  (void*)h->h_hc_count})
     if (p) (void)hipHostFree(p);
   delete h;
   return GK_OK;

@@ -531,22 +531,41 @@ __global__ __launch_bounds__(256) void k_presort(GKState st, const double* __res
   const int64_t total = list_b0[cnt];
   const int t = threadIdx.x;
   const int P = st.P;
-  for (int64_t gb = blockIdx.x; gb < total; gb += gridDim.x) {
-    // stream slot i: the last list_b0[i] <= gb
+  // a contiguous range of global batches per block: one binary search for
+  // its first stream slot, then the slot advances along the (ascending)
+  // list_b0 -- a search per batch was ~10 dependent global loads
+  const int64_t g0 = total * blockIdx.x / gridDim.x, g1 = total * (blockIdx.x + 1) / gridDim.x;
+  if (g0 >= g1) return;
+  int i = 0;
+  {
     int lo = 0, hi = cnt - 1;
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
-      if (list_b0[mid] <= gb) lo = mid;
+      if (list_b0[mid] <= g0) lo = mid;
       else hi = mid - 1;
     }
-    const int i = lo;
-    const int64_t wso = list_ws[i];
+    i = lo;
+  }
+  int64_t bnext = i + 1 < cnt ? list_b0[i + 1] : INT64_MAX;  // first global batch of slot i + 1
+  int ci = -1;  // the slot whose parameters are loaded
+  int64_t wso = -1, b0 = 0, s = 0, xo = 0, need = 0;
+  int p = 0;
+  for (int64_t gb = g0; gb < g1; ++gb) {
+    while (gb >= bnext) {  // (slots without batches are passed over)
+      ++i;
+      bnext = i + 1 < cnt ? list_b0[i + 1] : INT64_MAX;
+    }
+    if (i != ci) {
+      ci = i;
+      wso = list_ws[i];
+      b0 = list_b0[i];
+      s = list[i];
+      xo = offs[s];
+      p = st.pend[s];
+      need = P - (list_n[i] % P);
+    }
     if (wso < 0) continue;  // block-uniform
-    const int64_t b = gb - list_b0[i];
-    const int64_t s = list[i];
-    const int64_t xo = offs[s];
-    const int p = st.pend[s];
-    const int64_t need = P - (list_n[i] % P);
+    const int64_t b = gb - b0;
     const double* pb = st.pbuf + s * (int64_t)st.pmax;
     const int m = b == 0 ? p + (int)need : P;
     const int64_t xb = b == 0 ? xo : xo + need + (b - 1) * P;  // first x value of the batch (after pending)
@@ -583,6 +602,79 @@ __global__ __launch_bounds__(256) void k_presort(GKState st, const double* __res
   }
 }
 
+// streams walked one wave each by k_stats_long (more: 64 per wave); also the
+// host-walked chains' limit
+#ifndef GK_SL_BCAST
+#define GK_SL_BCAST 1024
+#endif
+
+// ===========================================================================
+// Host-walked chains.  The gk:54 `_avg` update is three dependent float64
+// roundings per value: ~37 cycles per value on one gfx950 lane (15.7 ns), so
+// a 10^7-value stream is a 157 ms chain however the batch is spread.  A host
+// core runs the same three roundings at ~3 cycles each, so the longest
+// streams' chains go to host cores (gk_capi.cpp, over pinned chunk copies)
+// while the GPU ingests; k_hc_prep picks them and snapshots their pre-call
+// state, k_hc_apply writes the host's results back.
+// ===========================================================================
+__global__ __launch_bounds__(256) void k_hc_prep(GKState st, const int64_t* __restrict__ offs,
+                                                 const int32_t* __restrict__ list,
+                                                 const int64_t* __restrict__ list_n,
+                                                 const int32_t* __restrict__ count, int64_t min_len, int rel_pct,
+                                                 int64_t budget_factor, GKHostChainRec* __restrict__ recs,
+                                                 int32_t* __restrict__ hc_count) {
+  __shared__ int64_t pre[GK_HC_MAX];
+  __shared__ int64_t lmax;
+  const int t = threadIdx.x;
+  const int cnt = *count;
+  // (the list is sorted longest first: k_long_prep sorts up to
+  // GK_SORT_LONG_MAX >= GK_SL_BCAST entries, so eligibility is a prefix)
+  const bool on = min_len > 0 && cnt > 0 && cnt <= GK_SL_BCAST;
+  if (t == 0) lmax = on ? offs[(int64_t)list[0] + 1] - offs[list[0]] : 0;
+  __syncthreads();
+  // a chain shorter than rel_pct % of the longest finishes on the device
+  // under the longest stream's flushes anyway
+  const int64_t need = max(min_len, (int64_t)((double)lmax * (double)rel_pct / 100.0));
+  int64_t s = 0, xo = 0, L = 0;
+  if (on && t < cnt) {
+    s = list[t];
+    xo = offs[s];
+    L = offs[s + 1] - xo;
+  }
+  pre[t] = (on && t < cnt && L >= need) ? L : 0;
+  __syncthreads();
+  // inclusive prefix sums of the eligible lengths (Hillis-Steele)
+  for (int o = 1; o < GK_HC_MAX; o <<= 1) {
+    const int64_t a = t >= o ? pre[t - o] : 0;
+    __syncthreads();
+    pre[t] += a;
+    __syncthreads();
+  }
+  const int64_t budget = budget_factor * lmax;
+  const bool take = on && t < cnt && L >= need && pre[t] <= budget;
+  // a prefix: count it with a block-wide ballot of `take`
+  __shared__ int32_t k;
+  if (t == 0) k = 0;
+  __syncthreads();
+  if (take) {
+    recs[t] = GKHostChainRec{s, xo, L, list_n[t], st.sum[s], st.avg[s], st.mn[s], st.mx[s]};
+    atomicAdd(&k, 1);
+  }
+  __syncthreads();
+  if (t == 0) *hc_count = k;
+}
+
+__global__ __launch_bounds__(256) void k_hc_apply(GKState st, const GKHostChainRec* __restrict__ recs,
+                                                  const int32_t* __restrict__ hc_count) {
+  const int t = threadIdx.x;
+  if (t >= *hc_count) return;
+  const GKHostChainRec r = recs[t];
+  st.sum[r.s] = r.sum;
+  st.avg[r.s] = r.avg;
+  st.mn[r.s] = r.mn;
+  st.mx[r.s] = r.mx;
+}
+
 // ===========================================================================
 // k_stats_long: gk:52-59 for the streams k_stats hands over (longer than
 // GK_STATS_LONG values).  The _avg update is three dependent float64
@@ -602,9 +694,6 @@ __global__ __launch_bounds__(256) void k_presort(GKState st, const double* __res
 // This kernel runs on a second HIP stream beside k_ingest, which rewrites n:
 // the pre-call n of every listed stream comes from list_n.
 // ===========================================================================
-#ifndef GK_SL_BCAST
-#define GK_SL_BCAST 1024
-#endif
 #define SL_BCAST_DEPTH 4
 #ifndef SL_DEPTH
 #define SL_DEPTH 7  // chunks in flight: 7 x 8 loads = 56 <= the 63 vmcnt can count
@@ -702,13 +791,16 @@ __global__ __launch_bounds__(64) void k_stats_long(GKState st, const double* __r
                                                    const int64_t* __restrict__ offs,
                                                    const int32_t* __restrict__ list,
                                                    const int64_t* __restrict__ list_n,
-                                                   const int32_t* __restrict__ count) {
+                                                   const int32_t* __restrict__ count,
+                                                   const int32_t* __restrict__ hc_count) {
   __shared__ double2 buf[64];
   __shared__ double rtile[64];
   const int lane = threadIdx.x;
   const int cnt = *count;
   if (cnt <= GK_SL_BCAST) {
-    for (int w = blockIdx.x; w < cnt; w += gridDim.x) stats_long_bcast(st, x, offs, list, list_n, w, lane, buf);
+    // the first *hc_count streams are walked on host cores (k_hc_prep)
+    const int w0 = hc_count ? *hc_count : 0;
+    for (int w = w0 + blockIdx.x; w < cnt; w += gridDim.x) stats_long_bcast(st, x, offs, list, list_n, w, lane, buf);
     return;
   }
   const int ngroups = (cnt + 63) / 64;
@@ -3651,12 +3743,30 @@ hipError_t gk_launch_presort(const GKState& st, const double* x, const int64_t* 
 }
 
 hipError_t gk_launch_stats_long(const GKState& st, const double* x, const int64_t* offs, const int32_t* long_list,
-                                const int64_t* long_n, const int32_t* long_count, hipStream_t stream) {
+                                const int64_t* long_n, const int32_t* long_count, const int32_t* hc_count,
+                                hipStream_t stream) {
   if (st.S <= 0) return hipSuccess;
   // the long-stream count is only known on the device: a fixed grid of waves
   // reads it (an empty list costs one short launch)
   hipLaunchKernelGGL(k_stats_long, dim3((unsigned)(num_cu() * 4)), dim3(64), 0, stream, st, x, offs, long_list,
-                     long_n, long_count);
+                     long_n, long_count, hc_count);
+  return hipGetLastError();
+}
+
+hipError_t gk_launch_hc_prep(const GKState& st, const int64_t* offs, const int32_t* long_list, const int64_t* long_n,
+                             const int32_t* long_count, int64_t min_len, int rel_pct, int64_t budget_factor,
+                             GKHostChainRec* recs, int32_t* hc_count, hipStream_t stream) {
+  static_assert(GK_HC_MAX == 256, "k_hc_prep: one thread per record");
+  if (st.S <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_hc_prep, dim3(1), dim3(GK_HC_MAX), 0, stream, st, offs, long_list, long_n, long_count, min_len,
+                     rel_pct, budget_factor, recs, hc_count);
+  return hipGetLastError();
+}
+
+hipError_t gk_launch_hc_apply(const GKState& st, const GKHostChainRec* recs, const int32_t* hc_count,
+                              hipStream_t stream) {
+  if (st.S <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_hc_apply, dim3(1), dim3(GK_HC_MAX), 0, stream, st, recs, hc_count);
   return hipGetLastError();
 }
 

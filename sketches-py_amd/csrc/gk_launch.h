@@ -95,8 +95,29 @@ hipError_t gk_launch_stats_short(const GKState& st, const double* x, const int64
 hipError_t gk_launch_presort(const GKState& st, const double* x, const int64_t* offs, const int32_t* long_list,
                              const int64_t* long_n, const int32_t* long_count, const GKPresort& ps,
                              hipStream_t stream);
+// hc_count (device, may be NULL): the first *hc_count list entries are
+// walked on host cores (gk_launch_hc_prep) and skipped here
 hipError_t gk_launch_stats_long(const GKState& st, const double* x, const int64_t* offs, const int32_t* long_list,
-                                const int64_t* long_n, const int32_t* long_count, hipStream_t stream);
+                                const int64_t* long_n, const int32_t* long_count, const int32_t* hc_count,
+                                hipStream_t stream);
+// Host-walked chains: the longest streams of the sorted
+// long list whose gk:52-59 chains run on host cores.  One record per stream:
+// the pre-call state from gk_launch_hc_prep, the final one written back by
+// the host and applied by gk_launch_hc_apply.
+struct GKHostChainRec {
+  int64_t s, xo, len, n;
+  double sum, avg, mn, mx;
+};
+#define GK_HC_MAX 256
+// takes list entries while len >= min_len and len >= rel_pct % of the
+// longest, at most GK_HC_MAX of them and budget_factor x (the longest length)
+// values in all, and only when the list is walked one wave per stream
+// (<= GK_SL_BCAST streams); min_len <= 0: none
+hipError_t gk_launch_hc_prep(const GKState& st, const int64_t* offs, const int32_t* long_list, const int64_t* long_n,
+                             const int32_t* long_count, int64_t min_len, int rel_pct, int64_t budget_factor,
+                             GKHostChainRec* recs, int32_t* hc_count, hipStream_t stream);
+hipError_t gk_launch_hc_apply(const GKState& st, const GKHostChainRec* recs, const int32_t* hc_count,
+                              hipStream_t stream);
 // quantiles of the listed streams from their committed tables (after the join)
 hipError_t gk_launch_query_list(const GKState& st, const int32_t* list, const int32_t* count, const GKQuery& q,
                                 hipStream_t stream);
