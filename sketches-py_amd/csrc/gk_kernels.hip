@@ -6,7 +6,7 @@
 // -ffp-contract=off: no FMA contraction of the reference's float64 formulas.
 //
 // Kernels
-//   k_stats      gk:52-59   lane per stream: n/_sum/_avg sequential chain, min/max
+//   k_stats_short / k_stats_long / stats role  gk:52-59   lane per stream: n/_sum/_avg sequential chain, min/max
 //   k_ingest     gk:60-109  wave per stream: flush schedule + closed-form
 //                           merge_compress of each flush, table kept in LDS
 //                           for the whole call
@@ -290,122 +290,17 @@ __device__ __forceinline__ GKRec* gk_table_ptr_cs(const GKState& st, int64_t s, 
   return c == 0 ? st.tab[0] + s * (int64_t)st.cap[0] : st.tab[c] + (int64_t)slot * st.cap[c];
 }
 
-// ===========================================================================
-// k_stats: gk:52-59 for every value of the streams up to GK_STATS_LONG values
-// (when the small-class launch does not walk them itself).  The _sum/_avg updates are a dependent
-// float64 chain in insertion order, so each stream's chain runs on one lane
-// (a 256-thread block = 256 streams).  The block stages its streams' values
-// through LDS in chunks of STATS_CHUNK values per stream: 16 lanes load one
-// stream's chunk as one contiguous 128-byte run (full HBM lines), then every
-// lane walks its own row.  The header n is NOT written here: k_ingest owns
-// n and runs after this kernel on the same HIP stream, so both read the
-// pre-call n.
-// ===========================================================================
-#define STATS_CHUNK 16
+// Streams up to GK_STATS_LONG values have their gk:52-59 chains walked by the
+// stats role of the small-class launch (P <= 128) or by k_stats_short;
+// longer ones by k_stats_long (or on host cores), beside the ingest.
 #ifndef GK_STATS_LONG
 #define GK_STATS_LONG 16384  // longer streams go to k_stats_long (64 per wave, on a second HIP stream)
 #endif
-#define STATS_ROW (STATS_CHUNK + 1)  // +1 double: lanes' rows start on different banks
-
-__global__ __launch_bounds__(256) void k_stats(GKState st, const double* __restrict__ x,
-                                               const int64_t* __restrict__ offs) {
-  // (the long streams were listed by k_lengths and are k_stats_long's: they
-  // are skipped here)
-  __shared__ double tile[256 * STATS_ROW];
-  __shared__ int64_t so[257];
-  __shared__ int64_t smax;
-  const int t = threadIdx.x;
-  const int64_t s0 = (int64_t)blockIdx.x * 256;
-  const int nstr = (int)min((int64_t)256, st.S - s0);
-  if (t < nstr) so[t] = offs[s0 + t];
-  if (t == 0) {
-    so[nstr] = offs[s0 + nstr];
-    smax = 0;
-  }
-  __syncthreads();
-  int64_t L = 0;
-  if (t < nstr) L = so[t + 1] - so[t];
-  if (L > GK_STATS_LONG) L = 0;  // walked by k_stats_long, not in this block's trip count
-  // block-uniform trip count: the longest stream of the block
-  atomicMax((unsigned long long*)&smax, (unsigned long long)L);
-  __syncthreads();
-  const int64_t maxL = smax;
-  // lengths only: the long list; the chains run in the small-class launch
-  if (maxL == 0) return;
-  const int64_t s = s0 + t;
-  int64_t n = 0;
-  double mn = 0, mx = 0, sm = 0, av = 0;
-  if (t < nstr) {
-    n = st.n[s];
-    mn = st.mn[s];
-    mx = st.mx[s];
-    sm = st.sum[s];
-    av = st.avg[s];
-  }
-  const int sub = t & 15;   // lane within a stream's 16-lane group
-  const int grp = t >> 4;   // 16 streams per load row
-  // this thread's 16 load slots: stream r*16+grp, value k0+sub (bounds read
-  // from LDS each time: keeping them in registers costs 64 VGPRs)
-  // chunk k0's values are loaded into registers while chunk k0-16 is walked
-  double rv[16];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int ls = min(r * 16 + grp, nstr);
-    const int64_t i = so[ls] + sub;
-    rv[r] = (i < so[min(ls + 1, nstr)]) ? x[i] : 0.0;
-  }
-  for (int64_t k0 = 0; k0 < maxL; k0 += STATS_CHUNK) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) tile[(r * 16 + grp) * STATS_ROW + sub] = rv[r];
-    __syncthreads();
-    if (k0 + STATS_CHUNK < maxL) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int ls = min(r * 16 + grp, nstr);
-        const int64_t i = so[ls] + k0 + STATS_CHUNK + sub;
-        rv[r] = (i < so[min(ls + 1, nstr)]) ? x[i] : 0.0;
-      }
-    }
-    if (t < nstr && L - k0 >= STATS_CHUNK) {
-      // a full chunk: the reciprocals 1.0/n (IEEE divisions, off the chain)
-      // first, then the dependent _sum/_avg chain, fully unrolled
-      double rc[STATS_CHUNK];
-#pragma unroll
-      for (int k = 0; k < STATS_CHUNK; ++k) rc[k] = 1.0 / (double)(n + 1 + k);
-#pragma unroll
-      for (int k = 0; k < STATS_CHUNK; ++k) {
-        const double v = tile[t * STATS_ROW + k];
-        sm = sm + v;                              // gk:53
-        av = av + (v - av) * rc[k];               // gk:54 (no FMA: -ffp-contract=off)
-        if (v < mn) mn = v;                       // gk:56-57 (strict: first occurrence kept)
-        if (v > mx) mx = v;                       // gk:58-59
-      }
-      n += STATS_CHUNK;                           // gk:52
-    } else if (t < nstr) {
-      const int kmax = (int)min((int64_t)STATS_CHUNK, L - k0);
-      for (int k = 0; k < kmax; ++k) {
-        const double v = tile[t * STATS_ROW + k];
-        n += 1;                                   // gk:52
-        sm = sm + v;                              // gk:53
-        av = av + (v - av) * (1.0 / (double)n);   // gk:54 (no FMA: -ffp-contract=off)
-        if (v < mn) mn = v;                       // gk:56-57 (strict: first occurrence kept)
-        if (v > mx) mx = v;                       // gk:58-59
-      }
-    }
-    __syncthreads();
-  }
-  if (t < nstr && L > 0) {
-    st.mn[s] = mn;
-    st.mx[s] = mx;
-    st.sum[s] = sm;
-    st.avg[s] = av;
-  }
-}
 
 // The long-stream list (streams past GK_STATS_LONG values, for k_long_prep /
 // k_stats_long) and the pre-call n snapshot st.n0 (read by the small-class
 // launch's stats role while its ingest waves rewrite st.n): one stream per
-// thread, no LDS (~6 us per 10^6 streams; as part of k_stats, whose 35 KiB
+// thread, no LDS (~6 us per 10^6 streams; as part of the former k_stats, whose 35 KiB
 // chain tile holds it to 4 blocks per CU, it took 28 us).
 __global__ __launch_bounds__(256) void k_lengths(GKState st, const int64_t* __restrict__ offs,
                                                  int32_t* __restrict__ long_list, int32_t* __restrict__ long_count) {
@@ -416,7 +311,7 @@ __global__ __launch_bounds__(256) void k_lengths(GKState st, const int64_t* __re
 }
 
 // ===========================================================================
-// k_long_prep: the long-stream list k_stats built (in atomic order) sorted by
+// k_long_prep: the long-stream list k_lengths built (in atomic order) sorted by
 // length, longest first (ties: lower stream id first), so that k_ingest and
 // k_stats_long start the longest sequential chains first; and the pre-call n
 // of every listed stream saved for k_stats_long, which runs beside k_ingest
@@ -425,6 +320,9 @@ __global__ __launch_bounds__(256) void k_lengths(GKState st, const int64_t* __re
 // correct, only less balanced).  Runs before k_ingest on the same HIP stream.
 // ===========================================================================
 #define GK_SORT_LONG_MAX 4096
+#ifndef GK_PRESORT_REL
+#define GK_PRESORT_REL 4  // presort streams with >= 1/GK_PRESORT_REL of the longest one's flushes
+#endif
 
 __global__ __launch_bounds__(1024) void k_long_prep(GKState st, const int64_t* __restrict__ offs,
                                                     int32_t* __restrict__ list, int64_t* __restrict__ list_n,
@@ -475,10 +373,16 @@ __global__ __launch_bounds__(1024) void k_long_prep(GKState st, const int64_t* _
   // = first slot offset (in doubles) or -1 (not presorted: the workspace is
   // too small -- the host grows it from *ws_need after the call), list_b0[i]
   // = the stream's first global batch index (for k_presort's block mapping).
+  // Only streams within a factor GK_PRESORT_REL of the longest one's flush
+  // count are presorted: they alone can be the call's critical path (an
+  // unsorted flush costs ~2-3x a presorted one), and sorting every listed
+  // stream's batches cost cfg5 ~17 ms ahead of the ingest.
   __shared__ int64_t part[1024];
+  __shared__ unsigned long long nbmax;
+  if (t == 0) nbmax = 0;
+  __syncthreads();
   const int per = (cnt + 1023) / 1024;
   const int i0 = t * per, i1 = min(i0 + per, cnt);
-  int64_t mine = 0;
   for (int i = i0; i < i1; ++i) {
     const int64_t s = list[i];
     int64_t nb = 0;
@@ -488,7 +392,14 @@ __global__ __launch_bounds__(1024) void k_long_prep(GKState st, const int64_t* _
       nb = L >= need ? 1 + (L - need) / st.P : 0;
     }
     list_b0[i] = nb;  // count for now
-    mine += nb;
+    atomicMax(&nbmax, (unsigned long long)nb);
+  }
+  __syncthreads();
+  const int64_t nb_min = (int64_t)(nbmax / GK_PRESORT_REL);
+  int64_t mine = 0;
+  for (int i = i0; i < i1; ++i) {
+    if (list_b0[i] < nb_min) list_b0[i] = 0;  // flushed unsorted
+    mine += list_b0[i];
   }
   part[t] = mine;
   __syncthreads();
@@ -680,7 +591,7 @@ __global__ __launch_bounds__(256) void k_hc_apply(GKState st, const GKHostChainR
 }
 
 // ===========================================================================
-// k_stats_long: gk:52-59 for the streams k_stats hands over (longer than
+// k_stats_long: gk:52-59 for the streams k_lengths lists (longer than
 // GK_STATS_LONG values).  The _avg update is three dependent float64
 // roundings per value, so a long stream's time is its chain latency.  Two
 // layouts, chosen on the device from the list length (the list comes sorted
@@ -791,30 +702,17 @@ __device__ __forceinline__ void stats_long_bcast(const GKState& st, const double
   wsync<false>();
 }
 
-__global__ __launch_bounds__(64) void k_stats_long(GKState st, const double* __restrict__ x,
-                                                   const int64_t* __restrict__ offs,
-                                                   const int32_t* __restrict__ list,
-                                                   const int64_t* __restrict__ list_n,
-                                                   const int32_t* __restrict__ count,
-                                                   const int32_t* __restrict__ hc_count) {
-  __shared__ double2 buf[64];
-  __shared__ double rtile[64];
-  const int lane = threadIdx.x;
-  const int cnt = *count;
-  if (cnt <= GK_SL_BCAST) {
-    // the first *hc_count streams are walked on host cores (k_hc_prep)
-    const int w0 = hc_count ? *hc_count : 0;
-    for (int w = w0 + blockIdx.x; w < cnt; w += gridDim.x) stats_long_bcast(st, x, offs, list, list_n, w, lane, buf);
-    return;
-  }
-  const int ngroups = (cnt + 63) / 64;
-  for (int gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
-    const int w = gi * 64 + lane;
-    const bool act = w < cnt;
-    const int64_t s = act ? (int64_t)list[w] : 0;
+// The group walk of the stats kernels: lane l walks the gk:52-59 chain of
+// stream s (act), starting at pre-call count n0, from a register ring of
+// aligned 16-byte loads (SL_DEPTH chunks of 16 values in flight).  A step
+// costs ~25 VALU for 64 chains.
+__device__ __forceinline__ void stats_group_walk(const GKState& st, const double* __restrict__ x,
+                                                 const int64_t* __restrict__ offs, const int64_t s, const bool act,
+                                                 const int64_t n0, const int lane, double* rtile) {
+  {
     const int64_t xo = act ? offs[s] : 0;
     int64_t rem = act ? offs[s + 1] - xo : 0;
-    int64_t n = act ? list_n[w] : 0;
+    int64_t n = n0;
     double mn = 0, mx = 0, sm = 0, av = 0;
     if (act) {
       mn = st.mn[s];
@@ -835,11 +733,11 @@ __global__ __launch_bounds__(64) void k_stats_long(GKState st, const double* __r
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) maxch = max(maxch, (int64_t)__shfl_xor(maxch, o, 64));
     const double2* __restrict__ p2 = (const double2*)p;
-    // loads past a lane's last chunk read the first aligned 16 values of the
-    // batch instead (in bounds: a listed stream alone has > 16384 values), so
-    // every refill load is unconditional and the wait before a slot is
-    // consumed stays partial
-    const double2* __restrict__ dummy = (const double2*)(x + ((((uintptr_t)x) & 8) ? 1 : 0));
+    // loads past a lane's last chunk read the start of st.rtab instead (1 MiB
+    // the set owns, 16-byte aligned; the values are never used), so every
+    // refill load is unconditional and the wait before a slot is consumed
+    // stays partial
+    const double2* __restrict__ dummy = (const double2*)st.rtab;
     double2 ring[SL_DEPTH][8];
 #pragma unroll
     for (int d = 0; d < SL_DEPTH; ++d) {
@@ -901,6 +799,53 @@ __global__ __launch_bounds__(64) void k_stats_long(GKState st, const double* __r
       st.sum[s] = sm;
       st.avg[s] = av;
     }
+  }
+}
+
+__global__ __launch_bounds__(64) void k_stats_long(GKState st, const double* __restrict__ x,
+                                                   const int64_t* __restrict__ offs,
+                                                   const int32_t* __restrict__ list,
+                                                   const int64_t* __restrict__ list_n,
+                                                   const int32_t* __restrict__ count,
+                                                   const int32_t* __restrict__ hc_count) {
+  __shared__ double2 buf[64];
+  __shared__ double rtile[64];
+  const int lane = threadIdx.x;
+  const int cnt = *count;
+  if (cnt <= GK_SL_BCAST) {
+    // the first *hc_count streams are walked on host cores (k_hc_prep)
+    const int w0 = hc_count ? *hc_count : 0;
+    for (int w = w0 + blockIdx.x; w < cnt; w += gridDim.x) stats_long_bcast(st, x, offs, list, list_n, w, lane, buf);
+    return;
+  }
+  const int ngroups = (cnt + 63) / 64;
+  for (int gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
+    const int w = gi * 64 + lane;
+    const bool act = w < cnt;
+    stats_group_walk(st, x, offs, act ? (int64_t)list[w] : 0, act, act ? list_n[w] : 0, lane, rtile);
+  }
+}
+
+// k_stats_short: the short streams' chains (up to GK_STATS_LONG values; the
+// longer ones are k_stats_long's) when the small-class launch does not walk
+// them (P > 128: cfg5), 64 consecutive streams per wave with the group walk
+// of k_stats_long.  A wave's trip count is its own longest stream, not a
+// 256-stream block's (Zipf lengths: the former k_stats block-uniform chunk loop took
+// ~9 ms of a cfg5 step ahead of the ingest launch).  Runs before k_ingest on
+// the same HIP stream: st.n is the pre-call n.
+__global__ __launch_bounds__(64) void k_stats_short(GKState st, const double* __restrict__ x,
+                                                    const int64_t* __restrict__ offs) {
+  __shared__ double rtile[64];
+  const int lane = threadIdx.x;
+  const int64_t ngroups = (st.S + 63) / 64;
+  for (int64_t gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
+    const int64_t s = gi * 64 + lane;
+    bool act = s < st.S;
+    if (act) {
+      const int64_t L = offs[s + 1] - offs[s];
+      act = L > 0 && L <= GK_STATS_LONG;
+    }
+    stats_group_walk(st, x, offs, act ? s : 0, act, act ? st.n[s] : 0, lane, rtile);
   }
 }
 
@@ -1444,7 +1389,7 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
   // `prio` -- the streams longer than GK_STATS_LONG values, longest first
   // (k_sort_long) -- so that the long sequential flush chains start at once;
   // items [npri, npri+count) are the launch's streams in order, minus those
-  // already taken from `prio` (the same length test k_stats applied).
+  // already taken from `prio` (the same length test k_lengths applied).
   if (count_ptr) count = *count_ptr;
   const int64_t npri = prio ? (int64_t)*prio_count : 0;
   const int64_t total = npri + count;
@@ -2758,7 +2703,7 @@ __device__ __attribute__((noinline)) double small_quantiles(SmallLDS<VPL>& L, in
 // 16-byte loads (the k_stats_long layout, shallower) -- and then join the
 // ingest hand-out.  Batches of 64 streams are handed out through `swork`.
 // Streams longer than GK_STATS_LONG are k_stats_long's (listed beforehand by
-// the lengths-only k_stats).  The ingest waves do not read _min/_max: a fused
+// the lengths-only k_lengths).  The ingest waves do not read _min/_max: a fused
 // query that needs them writes a marker that k_qfix resolves after the launch.
 #ifndef GK_FS_DEPTH
 #define GK_FS_DEPTH 2  // chunks of 8 values in flight per lane
@@ -2812,7 +2757,7 @@ __device__ __forceinline__ void fused_stats_role(const GKState& st, const double
     int64_t n = 0;
     double mn = 0, mx = 0, sm = 0, av = 0;
     if (act) {
-      n = st.n0[s];  // pre-call n (k_stats snapshot): st.n[s] may already be the ingest's
+      n = st.n0[s];  // pre-call n (k_lengths snapshot): st.n[s] may already be the ingest's
       mn = st.mn[s];
       mx = st.mx[s];
       sm = st.sum[s];
@@ -3838,8 +3783,9 @@ hipError_t gk_launch_stats(const GKState& st, const int64_t* offs, int32_t* long
 
 hipError_t gk_launch_stats_short(const GKState& st, const double* x, const int64_t* offs, hipStream_t stream) {
   if (st.S <= 0) return hipSuccess;
-  const int64_t grid = (st.S + 255) / 256;
-  hipLaunchKernelGGL(k_stats, dim3((unsigned)grid), dim3(256), 0, stream, st, x, offs);
+  const int64_t ngroups = (st.S + 63) / 64;
+  const int64_t grid = std::min<int64_t>(ngroups, (int64_t)num_cu() * 16);
+  hipLaunchKernelGGL(k_stats_short, dim3((unsigned)grid), dim3(64), 0, stream, st, x, offs);
   return hipGetLastError();
 }
 

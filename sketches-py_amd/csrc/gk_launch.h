@@ -66,7 +66,7 @@ hipError_t gk_launch_ingest_big(int cap, const GKState& st, const double* x, con
                                 hipStream_t stream);
 // `fused_stats` > 0: the small-class batch launch (x given, no list) also
 // walks the gk:52-59 stats of every stream of at most GK_STATS_LONG values,
-// in that many waves per CU (then requires the lengths-only k_stats before).
+// in that many waves per CU (then requires the lengths-only k_lengths before).
 // `prio` / `prio_count` (device, may be NULL): streams handed out first by the
 // capacity-class kernels (the long streams of the batch, longest first);
 // `psort` / `prio_ws`: their presorted flush batches (GKPresort), or NULL.
@@ -88,7 +88,7 @@ struct GKPresort {
 // the long-stream list + pre-call n (k_lengths), then k_long_prep
 hipError_t gk_launch_stats(const GKState& st, const int64_t* offs, int32_t* long_list, int64_t* long_n,
                            int32_t* long_count, const GKPresort& ps, hipStream_t stream);
-// gk:52-59 chains of the streams up to GK_STATS_LONG values (k_stats; the
+// gk:52-59 chains of the streams up to GK_STATS_LONG values (k_stats_short; the
 // long ones are k_stats_long's), when class 0 is not the small class
 hipError_t gk_launch_stats_short(const GKState& st, const double* x, const int64_t* offs, hipStream_t stream);
 // k_presort over the plan k_long_prep wrote (no-op without a workspace)
