@@ -382,7 +382,7 @@ int grow_pools(gk_set* h, hipStream_t s) {
     const int64_t cap = std::max<int64_t>(need + need / 8, 1 << 20);
     HIP_TRY(hipStreamSynchronize(s));
     HIP_TRY(hipStreamSynchronize(h->aux));
-    HIP_TRY(hipStreamSynchronize(h->aux2));
+    if (h->aux2) HIP_TRY(hipStreamSynchronize(h->aux2));
     if (h->ps.ws) (void)hipFree(h->ps.ws);
     h->ps.ws = nullptr;
     h->ps.ws_cap = 0;
@@ -594,17 +594,24 @@ int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s) {
   // unless the small-class launch walks them) and the presort of the long
   // streams' flush batches
   HIP_TRY(gk_launch_stats(h->st, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->ps, s));
+  // the longest chains to host cores: k_hc_prep picks them (k_stats_long
+  // skips them) ahead of the fork, so that `aux` holds nothing but
+  // k_stats_long and its waves reach the CUs before the ingest grid of this
+  // call (queued behind the pick and its copies they lost that race and ran
+  // ~3x longer beside the ingest: cfg4 x8 shards 82 -> 110 ms per step).  The
+  // records go to the host on the copy stream; the host walks the chains in
+  // stats_join, while the GPU ingests.
+  h->hc_active = false;
+  if (h->hc_min > 0)
+    HIP_TRY(gk_launch_hc_prep(h->st, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->hc_min, h->hc_rel,
+                              4 * (int64_t)h->hc_threads, h->d_hc, h->d_hc_count, s));
   HIP_TRY(hipEventRecord(h->ev_fork, s));
   HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_fork, 0));
-  // the longest chains to host cores (k_hc_prep picks them; k_stats_long
-  // skips them); the host walks them in stats_join, while the GPU ingests
-  h->hc_active = false;
   if (h->hc_min > 0) {
-    HIP_TRY(gk_launch_hc_prep(h->st, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->hc_min, h->hc_rel,
-                              4 * (int64_t)h->hc_threads, h->d_hc, h->d_hc_count, h->aux));
-    HIP_TRY(hipMemcpyAsync(h->h_hc_count, h->d_hc_count, sizeof(int32_t), hipMemcpyDeviceToHost, h->aux));
-    HIP_TRY(hipMemcpyAsync(h->h_hc, h->d_hc, GK_HC_MAX * sizeof(GKHostChainRec), hipMemcpyDeviceToHost, h->aux));
-    HIP_TRY(hipEventRecord(h->ev_hc, h->aux));
+    HIP_TRY(hipStreamWaitEvent(h->hc_copy, h->ev_fork, 0));
+    HIP_TRY(hipMemcpyAsync(h->h_hc_count, h->d_hc_count, sizeof(int32_t), hipMemcpyDeviceToHost, h->hc_copy));
+    HIP_TRY(hipMemcpyAsync(h->h_hc, h->d_hc, GK_HC_MAX * sizeof(GKHostChainRec), hipMemcpyDeviceToHost, h->hc_copy));
+    HIP_TRY(hipEventRecord(h->ev_hc, h->hc_copy));
     h->hc_x = x;
   }
   HIP_TRY(gk_launch_stats_long(h->st, x, offs, h->d_long_list, h->d_long_n, h->d_long_count,
@@ -892,7 +899,11 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
 
   okm &= hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking) == hipSuccess;
   okm &= hipStreamCreateWithFlags(&h->hc_copy, hipStreamNonBlocking) == hipSuccess;
-  okm &= hipStreamCreateWithFlags(&h->aux2, hipStreamNonBlocking) == hipSuccess;
+  // (aux2 only where the presort runs: every stream of a process shares the
+  // box's 4 hardware queues, and a set's idle stream still takes a slot in
+  // their round-robin -- with 8 sets of 3 streams the cfg4 shards' long
+  // chains landed behind the next shard's ingest)
+  if (h->P > 128 && !h->big[0]) okm &= hipStreamCreateWithFlags(&h->aux2, hipStreamNonBlocking) == hipSuccess;
   okm &= hipEventCreateWithFlags(&h->ev_presort, hipEventDisableTiming) == hipSuccess;
   okm &= hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) == hipSuccess;
   okm &= hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) == hipSuccess;

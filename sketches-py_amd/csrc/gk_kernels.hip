@@ -321,7 +321,7 @@ __global__ __launch_bounds__(256) void k_lengths(GKState st, const int64_t* __re
 // ===========================================================================
 #define GK_SORT_LONG_MAX 4096
 #ifndef GK_PRESORT_REL
-#define GK_PRESORT_REL 4  // presort streams with >= 1/GK_PRESORT_REL of the longest one's flushes
+#define GK_PRESORT_REL 3  // presort streams with >= 1/GK_PRESORT_REL of the longest one's flushes
 #endif
 
 __global__ __launch_bounds__(1024) void k_long_prep(GKState st, const int64_t* __restrict__ offs,
