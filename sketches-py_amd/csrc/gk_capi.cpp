@@ -504,6 +504,9 @@ int run_host_chains(gk_set* h, int* taken) {
   HIP_TRY(hipEventSynchronize(h->ev_hc));
   const int K = std::min(*h->h_hc_count, GK_HC_MAX);
   if (K <= 0) return GK_OK;
+  // the picked records (k_hc_prep, complete: ev_hc followed it)
+  HIP_TRY(hipMemcpyAsync(h->h_hc, h->d_hc, K * sizeof(GKHostChainRec), hipMemcpyDeviceToHost, h->hc_copy));
+  HIP_TRY(hipStreamSynchronize(h->hc_copy));
   const int T = std::max(1, std::min(h->hc_threads, K));
   int rc = hc_ensure(h, T);
   if (rc) return rc;
@@ -602,18 +605,18 @@ int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s) {
   // records go to the host on the copy stream; the host walks the chains in
   // stats_join, while the GPU ingests.
   h->hc_active = false;
-  if (h->hc_min > 0)
+  if (h->hc_min > 0) {
+    // (only the pick's count comes back here; the records follow in
+    // run_host_chains when there are any -- every stream of the process
+    // shares 4 hardware queues, and copies queued beside `aux` delayed it)
     HIP_TRY(gk_launch_hc_prep(h->st, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->hc_min, h->hc_rel,
                               4 * (int64_t)h->hc_threads, h->d_hc, h->d_hc_count, s));
-  HIP_TRY(hipEventRecord(h->ev_fork, s));
-  HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_fork, 0));
-  if (h->hc_min > 0) {
-    HIP_TRY(hipStreamWaitEvent(h->hc_copy, h->ev_fork, 0));
-    HIP_TRY(hipMemcpyAsync(h->h_hc_count, h->d_hc_count, sizeof(int32_t), hipMemcpyDeviceToHost, h->hc_copy));
-    HIP_TRY(hipMemcpyAsync(h->h_hc, h->d_hc, GK_HC_MAX * sizeof(GKHostChainRec), hipMemcpyDeviceToHost, h->hc_copy));
-    HIP_TRY(hipEventRecord(h->ev_hc, h->hc_copy));
+    HIP_TRY(hipMemcpyAsync(h->h_hc_count, h->d_hc_count, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipEventRecord(h->ev_hc, s));
     h->hc_x = x;
   }
+  HIP_TRY(hipEventRecord(h->ev_fork, s));
+  HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_fork, 0));
   HIP_TRY(gk_launch_stats_long(h->st, x, offs, h->d_long_list, h->d_long_n, h->d_long_count,
                                h->hc_min > 0 ? h->d_hc_count : nullptr, h->aux));
   h->hc_active = h->hc_min > 0;  // (stats_join walks the picked chains)
