@@ -148,11 +148,11 @@ struct gk_set {
   hipEvent_t ev_hc = nullptr;       // the records' D2H copy
   bool hc_active = false;           // this call enqueued k_hc_prep
   const double* hc_x = nullptr;     // the call's values
-  // one copy stream for every host thread's chunk copies, made right after
-  // `aux` so that it gets a hardware queue of its own (the box runs 4 per
-  // process: a copy stream sharing the ingest's or aux's queue waits behind
-  // their kernels -- 16 per-thread streams gave 12 GB/s instead of ~55);
-  // per host thread two pinned chunk buffers and their events
+  // one copy stream for every host thread's chunk copies, made at the first
+  // host-walked chain (the box runs 4 hardware queues per process: a copy
+  // stream sharing the ingest's or aux's queue waits behind their kernels --
+  // 16 per-thread streams gave 12 GB/s instead of ~55); per host thread two
+  // pinned chunk buffers and their events
   hipStream_t hc_copy = nullptr;
   // k_presort of the long streams' flush batches runs here beside the short
   // streams' chains (k_stats on the caller's stream); the ingest waits for it
@@ -504,6 +504,7 @@ int run_host_chains(gk_set* h, int* taken) {
   HIP_TRY(hipEventSynchronize(h->ev_hc));
   const int K = std::min(*h->h_hc_count, GK_HC_MAX);
   if (K <= 0) return GK_OK;
+  if (!h->hc_copy) HIP_TRY(hipStreamCreateWithFlags(&h->hc_copy, hipStreamNonBlocking));
   // the picked records (k_hc_prep, complete: ev_hc followed it)
   HIP_TRY(hipMemcpyAsync(h->h_hc, h->d_hc, K * sizeof(GKHostChainRec), hipMemcpyDeviceToHost, h->hc_copy));
   HIP_TRY(hipStreamSynchronize(h->hc_copy));
@@ -901,7 +902,10 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
   okm &= hipMalloc(&h->d_long_n, S * sizeof(int64_t)) == hipSuccess;
 
   okm &= hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking) == hipSuccess;
-  okm &= hipStreamCreateWithFlags(&h->hc_copy, hipStreamNonBlocking) == hipSuccess;
+  // (hc_copy is made on first use, run_host_chains: an idle stream still
+  // takes a slot in the round-robin over the box's 4 hardware queues, and
+  // with 8 sets the long chains' `aux` then shared the caller's queue more
+  // often)
   // (aux2 only where the presort runs: every stream of a process shares the
   // box's 4 hardware queues, and a set's idle stream still takes a slot in
   // their round-robin -- with 8 sets of 3 streams the cfg4 shards' long
