@@ -10,9 +10,16 @@ quantiles([0.5, 0.9, 0.99]) for every stream: k_stats (n/sum/avg/min/max
 chain) then one k_ingest pass (9 automatic flushes per stream at the
 reference's flush points, then the query flush of the 91 pending values,
 gk:197, and the rank walk from the on-chip table).  Inputs are generated on the GPU (synthetic, seeded)
-and are resident in HBM before the timed region.  Multi-GPU: every rank runs
-its own 1M-stream shard (streams are independent: weak scaling, no collective
-on the data path); value = all ranks' values / max-over-ranks time.
+and are resident in HBM before the timed region.
+
+Multi-GPU (one process per GPU, streams are independent: no collective on the
+data path).  Default for N > 1 is the metric's configuration, STRONG split:
+the one 1M-stream cfg3 batch (the same seeded batch a single GPU runs) is
+split by ``dist.stream_range`` into N contiguous stream ranges, one per rank
+(cfg5: ``dist.balanced_assignment`` by stream length, longest first); value =
+the batch's values / max-over-ranks time.  The weak line (every rank its own
+1M streams, seed + rank) is measured in the same run and reported beside it
+under "weak" (``--split weak`` makes it the headline; ``--no-weak`` skips it).
 
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
@@ -58,6 +65,14 @@ def parse():
                     help="also time the host engine on every CPU of the affinity set (beyond this job's share)")
     ap.add_argument("--exchange", default="allgather", choices=["allgather", "alltoall"],
                     help="cfg4 row-shard exchange over RCCL before the merge fold")
+    ap.add_argument("--split", default="auto", choices=["auto", "strong", "weak"],
+                    help="N > 1, cfg2/3/5: strong = split the one batch over the ranks by stream "
+                         "(the metric's configuration; the default), weak = every rank its own batch")
+    ap.add_argument("--no-weak", action="store_true", help="N > 1 strong: skip the weak line beside it")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu = the host engine (libgkarray_cpu.so): split / dump checks on CPU only")
+    ap.add_argument("--dump", default=None,
+                    help="write this rank's quantiles and global stream ids to DUMP.rank<r>.npz (tests)")
     ap.add_argument("--virtual-shards", type=int, default=1,
                     help="cfg4 on one process: sketch K row shards on this GPU and fold them with "
                          "GKArray.merge in shard order (the merge work of a K-GPU run, without the exchange)")
@@ -214,18 +229,59 @@ def cpu_baseline(x, offs, sample, threads, eps, gpu_q, py_streams=2000, all_core
     return out
 
 
+def sub_batch(x, offs, idx):
+    """Streams `idx` (ascending global ids, int64 CPU tensor) of the CSR batch
+    (x, offs) as a contiguous CSR batch of their own, values in the same
+    order: a slice when the ids are one range (cfg3 strong split), else a
+    gather (cfg5's balanced assignment)."""
+    dev = x.device
+    k = int(idx.numel())
+    if k == 0:
+        return torch.zeros(1, dtype=torch.float64, device=dev), torch.zeros(1, dtype=torch.int64, device=dev)
+    lo, hi = int(idx[0]), int(idx[-1]) + 1
+    if hi - lo == k:
+        a, b = int(offs[lo].item()), int(offs[hi].item())
+        return x[a:b].clone(), (offs[lo:hi + 1] - a).contiguous()
+    i_d = idx.to(dev)
+    starts = offs[i_d]
+    lens = offs[i_d + 1] - starts
+    o = torch.zeros(k + 1, dtype=torch.int64, device=dev)
+    o[1:] = torch.cumsum(lens, 0)
+    tot = int(o[-1].item())
+    seg = torch.repeat_interleave(torch.arange(k, device=dev), lens)
+    pos = starts[seg] + (torch.arange(tot, device=dev) - o[:-1][seg])
+    return x[pos].contiguous(), o
+
+
+def rank_streams(workload, offs, world, rank):
+    """This rank's streams of the one batch (strong split): a contiguous
+    `stream_range` (cfg2 / cfg3: equal lengths), or the longest-first
+    `balanced_assignment` by stream length (cfg5's Zipf lengths)."""
+    from gkarray_amd import dist as gd
+    S = offs.numel() - 1
+    if workload == "cfg5":
+        lens = (offs[1:] - offs[:-1]).cpu()
+        return gd.balanced_assignment(lens, world)[rank]
+    a, b = gd.stream_range(S, world, rank)
+    return torch.arange(a, b, dtype=torch.int64)
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    on_gpu = a.device == "cuda"
     # GK_BENCH_REHEARSE=1: rehearse the N-rank path on fewer GPUs (ranks share
     # devices, gloo for the timing collectives; the numbers mean nothing)
-    rehearse = os.environ.get("GK_BENCH_REHEARSE") == "1"
-    if rehearse:
-        local %= max(torch.cuda.device_count(), 1)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    rehearse = os.environ.get("GK_BENCH_REHEARSE") == "1" or not on_gpu
+    if on_gpu:
+        if rehearse:
+            local %= max(torch.cuda.device_count(), 1)
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    else:
+        dev = torch.device("cpu")
     if world > 1:
         import torch.distributed as dist
         if rehearse:
@@ -233,6 +289,23 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=dev)
     from gkarray_amd import StreamSet
+
+    def gsync():
+        if on_gpu:
+            torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    def allreduce(v, op):
+        if world == 1:
+            return v
+        import torch.distributed as dist
+        t = torch.tensor([v], dtype=torch.float64, device="cpu" if rehearse else dev)
+        dist.all_reduce(t, op=op)
+        return float(t.item())
 
     defaults = {"cfg3": (1_000_000, 1000, "pareto"), "cfg2": (100_000, 10_000, "lognormal"),
                 "cfg4": (10_000, 1_000_000, "lognormal"), "cfg5": (100_000, 0, "zipf-lengths lognormal")}
@@ -242,6 +315,43 @@ def main():
     if a.eps is None:
         a.eps = 0.001 if a.workload == "cfg5" else 0.01
     qs = [0.5, 0.9, 0.99]
+    split = a.split if a.split != "auto" else ("strong" if world > 1 else "weak")
+    if a.workload == "cfg4":
+        split = "rows"
+
+    def make_batch(seed):
+        if a.workload == "cfg5":
+            return make_zipf_input(S, seed, dev, cap=a.values or 10_000_000)
+        return make_input(S, L, seed, dev, dist_name)
+
+    def timed(step, timed_sets):
+        """W untimed steps, then K steps bracketed by barrier + device sync;
+        (max-over-ranks seconds, launch ms summed over sets, stats ms, launches, last result)."""
+        for _ in range(a.warmup):
+            step()
+        gsync()
+        for t_ss in timed_sets:
+            t_ss.timing(True)
+            t_ss.read_timing()
+        barrier()
+        gsync()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            q = step()
+        gsync()
+        barrier()
+        dt = time.perf_counter() - t0
+        f_ms = s_ms = 0.0
+        n_l = 0
+        for t_ss in timed_sets:  # every shard's ingest launches (cfg4 virtual shards)
+            f, s_, n = t_ss.read_timing()
+            t_ss.timing(False)
+            f_ms, s_ms, n_l = f_ms + f, s_ms + s_, n_l + n
+        import torch.distributed as _d
+        return allreduce(dt, _d.ReduceOp.MAX) if world > 1 else dt, f_ms, s_ms, n_l, q
+
+    K = 1
+    idx = None
     if a.workload == "cfg4":
         # rows of every stream split over the ranks: this rank sketches its
         # L/world values of each of the S streams, then the shards are merged
@@ -249,6 +359,7 @@ def main():
         K = max(1, a.virtual_shards) if world == 1 else 1
         L = L // (world * K)
         N = S * L * K
+        S_loc = S
         if K == 1:
             x, offs = make_input(S, L, a.seed + rank, dev, dist_name)
             ss = StreamSet(S, a.eps, device=dev)
@@ -271,14 +382,18 @@ def main():
                 sets[0].merge_from(sets[1:])  # sk0.merge(sk1)...merge(skK-1), gk:111-154
                 return sets[0].quantiles(qs)
     else:
-        if a.workload == "cfg5":
-            x, offs = make_zipf_input(S, 5 + rank, dev, cap=a.values or 10_000_000)
-            N = x.numel()
-            L = N / S  # mean length
+        if split == "strong":
+            # the one batch every rank would run alone (same seed on every
+            # rank), cut to this rank's streams
+            x_full, offs_full = make_batch(5 if a.workload == "cfg5" else a.seed)
+            idx = rank_streams(a.workload, offs_full, world, rank)
+            x, offs = sub_batch(x_full, offs_full, idx)
+            del x_full, offs_full
         else:
-            N = S * L
-            x, offs = make_input(S, L, a.seed + rank, dev, dist_name)
-        ss = StreamSet(S, a.eps, device=dev)
+            x, offs = make_batch((5 if a.workload == "cfg5" else a.seed) + rank)
+        S_loc = offs.numel() - 1
+        N = int(offs[-1].item())
+        ss = StreamSet(S_loc, a.eps, device=dev)
 
         def step():
             ss.reset()
@@ -286,7 +401,7 @@ def main():
             # enqueued without a host synchronisation (the timed region syncs at its end)
             return ss.ingest(x, offs, quantiles=qs, sync=False)
 
-    # algorithmic bytes of one k_ingest launch (untimed identical step)
+    # algorithmic bytes of one k_ingest_small launch (untimed identical step)
     timed_sets = [ss]
     if a.workload == "cfg4" and K > 1:
         # one shard's ingest launch (before the merges flush the sets)
@@ -297,46 +412,42 @@ def main():
         step()
     else:
         step()
-        bytes_per_launch = algorithmic_bytes(ss, S, N, len(qs) if a.workload != "cfg4" else 0)
+        bytes_per_launch = algorithmic_bytes(ss, S_loc, N, len(qs) if a.workload != "cfg4" else 0)
 
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
-
-    def barrier():
-        if world > 1:
-            import torch.distributed as dist
-            dist.barrier()
-
-    for t_ss in timed_sets:
-        t_ss.timing(True)
-        t_ss.read_timing()
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        q = step()
-    torch.cuda.synchronize()
-    barrier()
-    dt = time.perf_counter() - t0
-    flush_ms = stats_ms = 0.0
-    launches = 0
-    for t_ss in timed_sets:  # every shard's ingest launches (cfg4 virtual shards)
-        f_ms, s_ms, n_l = t_ss.read_timing()
-        t_ss.timing(False)
-        flush_ms, stats_ms, launches = flush_ms + f_ms, stats_ms + s_ms, launches + n_l
-    if world > 1:
-        import torch.distributed as dist
-        t = torch.tensor([dt], dtype=torch.float64, device="cpu" if rehearse else dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    import torch.distributed as _d
+    dt, flush_ms, stats_ms, launches, q = timed(step, timed_sets)
+    if a.dump:
+        np.savez("%s.rank%d.npz" % (a.dump, rank), q=q.cpu().numpy(),
+                 idx=(idx if idx is not None else torch.arange(S_loc)).numpy())
 
     traffic, traffic_src = pmc_traffic(a.workload)
-    total_values = N * world * a.steps
+    if traffic is not None and (not on_gpu or S_loc != defaults[a.workload][0] or
+                                (a.workload != "cfg5" and L != defaults[a.workload][1])):
+        traffic, traffic_src = None, "the PMC profile is of the whole single-GPU workload, not this batch"
+    total_values = allreduce(float(N), _d.ReduceOp.SUM) * a.steps if world > 1 else N * a.steps
     value = total_values / dt
     ms_step = dt / a.steps * 1e3
     k_ms = flush_ms / max(launches, 1)
-    achieved = bytes_per_launch / (k_ms * 1e-3) / 1e9
+    achieved = bytes_per_launch / (k_ms * 1e-3) / 1e9 if k_ms > 0 else None
+    ratio = traffic / bytes_per_launch if traffic else None
+    if a.workload == "cfg4":
+        parallelism = ("row-sharded x%d, RCCL %s + merge" % (world, a.exchange) if K == 1 else
+                       "row-sharded: %d virtual shards on 1 GPU, merge fold (no exchange)" % K)
+        workload = ("cfg4: %d streams x %d values, row-sharded %d values per stream per shard "
+                    "(%d GPU x %d shard), eps=%g, ingest + %s + rank-ordered merge + quantiles"
+                    % (S, L * world * K, L, world, K, a.eps, a.exchange))
+    else:
+        lens_txt = ("%d" % L) if a.workload != "cfg5" else "clip(zipf(1.5),1,1e7)"
+        if split == "strong":
+            parallelism = ("stream-sharded, strong: the one %d-stream batch split over %d rank(s) by %s "
+                           "(no collective)" % (S, world, "balanced_assignment (longest first)"
+                                                if a.workload == "cfg5" else "stream_range"))
+            workload = ("%s: %d streams x %s values (one batch, node), %d on this rank, eps=%g, %s, "
+                        "ingest + quantiles(.5,.9,.99)" % (a.workload, S, lens_txt, S_loc, a.eps, dist_name))
+        else:
+            parallelism = "stream-sharded x%d, weak: every rank its own batch (no collective)" % world
+            workload = ("%s: %d streams x %s values per GPU, eps=%g, %s, ingest + quantiles(.5,.9,.99)"
+                        % (a.workload, S, lens_txt, a.eps, dist_name))
     line = {
         "metric": "values ingested/sec (node) @1M streams eps=0.01; % of HBM roofline",
         "value": value,
@@ -346,30 +457,44 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": ms_step,
         "higher_is_better": True,
-        "scaling": "weak" if a.workload != "cfg4" else "strong",
+        "scaling": "weak" if split == "weak" else "strong",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic: %s float64 generated on GPU (seed %d + rank)" % (
-            "Pareto(1.5)+1" if dist_name == "pareto" else "lognormal(0,1)", a.seed),
-        "config": {"workload": ("%s: %d streams x %s values per GPU, eps=%g, %s, ingest + quantiles(.5,.9,.99)"
-                                % (a.workload, S, ("%d" % L) if a.workload != "cfg5" else
-                                   ("clip(zipf(1.5),1,1e7) (%d total)" % N), a.eps, dist_name))
-                               if a.workload != "cfg4" else
-                               ("cfg4: %d streams x %d values, row-sharded %d values per stream per shard "
-                                "(%d GPU x %d shard), eps=%g, ingest + %s + rank-ordered merge + quantiles"
-                                % (S, L * world * K, L, world, K, a.eps, a.exchange)),
-                   "streams_per_gpu": S, "values_per_stream": L, "eps": a.eps,
-                   "parallelism": ("stream-sharded x%d (no collective)" % world) if a.workload != "cfg4"
-                   else ("row-sharded x%d, RCCL %s + merge" % (world, a.exchange) if K == 1 else
-                         "row-sharded: %d virtual shards on 1 GPU, merge fold (no exchange)" % K)},
-        "roofline": {"bound": "hbm", "kernel": "k_ingest", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_source": traffic_src,
+        "data": "synthetic: %s float64 generated on %s (seed %d%s)" % (
+            "Pareto(1.5)+1" if dist_name == "pareto" else "lognormal(0,1)", "GPU" if on_gpu else "CPU",
+            5 if a.workload == "cfg5" else a.seed, " + rank" if split in ("weak", "rows") else ", one batch"),
+        "config": {"workload": workload, "split": split,
+                   "streams_per_gpu": S_loc, "values_per_stream": L if a.workload != "cfg5" else N / max(S_loc, 1),
+                   "eps": a.eps,
+                   "parallelism": parallelism},
+        "roofline": {"bound": "hbm", "kernel": "k_ingest_small" if a.workload != "cfg5" else "k_ingest",
+                     "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
+                     "traffic_ratio": ratio, "traffic_source": traffic_src,
                      "bytes_per_launch": bytes_per_launch, "launch_ms": k_ms,
                      "stats_kernel_ms": stats_ms / max(launches, 1)},
         "library": _library_identity(),
     }
-    if rank == 0 and world == 1 and not a.no_cpu and a.workload != "cfg4":
+    if not on_gpu:
+        line["device"] = "cpu (host engine libgkarray_cpu.so): a split check, not a GPU number"
+    if world > 1 and split == "strong" and not a.no_weak:
+        # the weak line beside it: every rank its own whole batch (seed + rank)
+        del ss, x, offs, q
+        xw, ow = make_batch((5 if a.workload == "cfg5" else a.seed) + rank)
+        nw = int(ow[-1].item())
+        sw = StreamSet(ow.numel() - 1, a.eps, device=dev)
+
+        def step_w():
+            sw.reset()
+            return sw.ingest(xw, ow, quantiles=qs, sync=False)
+
+        step_w()
+        dtw, fw, _, lw, _ = timed(step_w, [sw])
+        tot_w = allreduce(float(nw), _d.ReduceOp.SUM) * a.steps
+        line["weak"] = {"value": tot_w / dtw, "ms_per_step": dtw / a.steps * 1e3, "scaling": "weak",
+                        "streams_per_gpu": S, "launch_ms": fw / max(lw, 1),
+                        "note": "every rank its own %d-stream batch (seed + rank), same K/W" % S}
+    if rank == 0 and world == 1 and on_gpu and not a.no_cpu and a.workload != "cfg4":
         threads = a.cpu_threads or host_cores()[0]
         sample = min(a.cpu_sample, S)
         if a.workload == "cfg5":  # the long streams dominate: a bounded prefix of streams
