@@ -200,6 +200,11 @@ double gk_eps(const gk_set* set);
 int gk_flush_period(const gk_set* set);       /* int(1.0/eps) + 1 (gk:60)  */
 int gk_capacity(const gk_set* set, int cls);  /* table capacity of a class */
 int64_t gk_num_promoted(const gk_set* set);   /* streams in the large class */
+/* Streams whose gk:52-59 chains the host walked in the last completed
+ * ingest (host-walked chains; 0 when none were picked or
+ * the walk failed and the device walked them), -1 for a bad set.  Waits for
+ * the set's host worker.  Diagnostics only: results never depend on it. */
+int64_t gk_host_chains_taken(gk_set* set);
 
 /* Kernel timing: when enabled, gk_ingest records HIP events around the flush
  * kernel it launches on `stream`; gk_timing_read returns the summed

@@ -776,6 +776,7 @@ int gk_fold_packed(gk_set* dst, const void* const* bufs, int nbufs, void* stream
 int gk_flush_period(const gk_set* h) { return h ? (int)std::min<int64_t>(h->P, INT32_MAX) : -1; }
 int gk_capacity(const gk_set* h, int cls) { return (h && cls == 0) ? INT32_MAX : -1; }  // unbounded, one class
 int64_t gk_num_promoted(const gk_set* h) { return h ? 0 : -1; }
+int64_t gk_host_chains_taken(gk_set* h) { return h ? 0 : -1; }  // the host engine walks every chain itself
 
 int gk_timing_enable(gk_set* h, int on) {
   int rc = check_set(h);

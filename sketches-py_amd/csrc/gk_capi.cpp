@@ -16,6 +16,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -147,7 +150,9 @@ struct gk_set {
   int32_t* h_hc_count = nullptr;
   hipEvent_t ev_hc = nullptr;       // the records' D2H copy
   bool hc_active = false;           // this call enqueued k_hc_prep
-  const double* hc_x = nullptr;     // the call's values
+  const double* hc_x = nullptr;     // the call's values and offsets
+  const int64_t* hc_offs = nullptr;
+  bool forked = false;              // stats_fork launched on aux; stats_join / stats_abort joins it
   // one copy stream for every host thread's chunk copies, made at the first
   // host-walked chain (the box runs 4 hardware queues per process: a copy
   // stream sharing the ingest's or aux's queue waits behind their kernels --
@@ -161,6 +166,26 @@ struct gk_set {
   std::vector<hipStream_t> hc_streams;
   std::vector<double*> hc_buf;
   std::vector<hipEvent_t> hc_ev;
+  // The host walk is asynchronous (round 4): gk_ingest* only hands the call
+  // to a worker thread of the set and enqueues the join on the caller's
+  // stream (k_hc_wait on a pinned flag the worker writes, then the records'
+  // copy, k_hc_apply, and k_hc_fallback which walks the picked chains on the
+  // device if the host walk failed).  The next call on the set (or gk_sync /
+  // gk_destroy) waits for the worker first, so the call's input buffers are
+  // read by the worker no longer than the header's contract allows.
+  std::thread hc_thr;
+  std::mutex hc_mu;
+  std::condition_variable hc_cv;
+  std::deque<uint64_t> hc_jobs;             // calls whose chains wait for the worker
+  bool hc_stop = false;
+  uint64_t hc_seq = 0;                      // sequence number of the last handed-out call
+  unsigned long long* h_hc_flag = nullptr;  // pinned, device-visible: (seq << 2) | 1 done / 2 failed
+  int32_t* d_hc_fail = nullptr;             // device: this call's walk failed (set by k_hc_wait)
+  int hc_fail_inject = 0;                   // GK_HC_FAIL=1 (tests): the worker reports a failure
+  double hc_timeout_s = 20.0;               // k_hc_wait's bound on the host walk
+  int64_t hc_last_taken = 0;                // streams the host walked in the last completed job
+  int hc_last_rc = GK_OK;
+  std::string hc_last_msg;
   // timing: event pairs recorded around the timed launches, summed at read
   bool timing = false;
   std::vector<hipEvent_t> tev_flush, tev_stats;
@@ -354,10 +379,13 @@ int replay_deferred(gk_set* h, hipStream_t s) {
   return fail(GK_E_OVERFLOW, "deferred streams could not be placed in a capacity class");
 }
 
+void hc_drain(gk_set* h);
+
 // Before a call (and in gk_sync): settle the previous call -- wait for it when
 // it may have deferred streams (some class could run out of slots), re-run
 // those, report its asynchronous errors.
 int settle(gk_set* h, hipStream_t s, bool block) {
+  hc_drain(h);  // the last call's host walk reads its inputs: done before anything else
   poll(h, block || h->last.may_defer);
   if (h->done_pending) return GK_OK;  // still running, and it cannot have deferred anything
   return replay_deferred(h, s);
@@ -589,6 +617,75 @@ int run_host_chains(gk_set* h, int* taken) {
   return GK_OK;
 }
 
+// The set's host-walk worker: walks the chains of each handed-out call (in
+// order), then publishes (seq << 2) | status in the pinned flag that the
+// call's k_hc_wait reads -- always, on failure too (status 2: k_hc_fallback
+// then walks those streams on the device).
+void hc_worker_main(gk_set* h) {
+  (void)hipSetDevice(h->device);
+  for (;;) {
+    uint64_t seq = 0;
+    {
+      std::unique_lock<std::mutex> lk(h->hc_mu);
+      h->hc_cv.wait(lk, [h] { return h->hc_stop || !h->hc_jobs.empty(); });
+      if (h->hc_jobs.empty()) return;  // stop, nothing left
+      seq = h->hc_jobs.front();
+    }
+    int taken = 0;
+    int rc = run_host_chains(h, &taken);
+    std::string msg = rc ? g_err : std::string();
+    if (!rc && h->hc_fail_inject) {
+      rc = GK_E_HIP;
+      taken = 0;
+      msg = "host-walked chains: failure injected (GK_HC_FAIL)";
+    }
+    __atomic_store_n(h->h_hc_flag, (unsigned long long)((seq << 2) | (rc == GK_OK ? 1u : 2u)), __ATOMIC_RELEASE);
+    {
+      std::lock_guard<std::mutex> lk(h->hc_mu);
+      h->hc_jobs.pop_front();
+      h->hc_last_taken = taken;
+      h->hc_last_rc = rc;
+      h->hc_last_msg = msg;
+    }
+    h->hc_cv.notify_all();
+  }
+}
+
+// Wait until the worker has walked every handed-out call (start of the next
+// call, gk_sync, gk_destroy).  A failed walk is not an error of the set: the
+// device walked those chains instead (k_hc_fallback).
+void hc_drain(gk_set* h) {
+  if (!h->hc_thr.joinable()) return;
+  std::unique_lock<std::mutex> lk(h->hc_mu);
+  h->hc_cv.wait(lk, [h] { return h->hc_jobs.empty(); });
+}
+
+void hc_shutdown(gk_set* h) {
+  if (!h->hc_thr.joinable()) return;
+  {
+    std::lock_guard<std::mutex> lk(h->hc_mu);
+    h->hc_stop = true;
+  }
+  h->hc_cv.notify_all();
+  h->hc_thr.join();
+}
+
+// A call that fails between stats_fork and stats_join: best effort, `s` still
+// waits for the aux work, and chains the host would have walked are walked on
+// the device (k_hc_fallback with the fail word set).
+void stats_abort(gk_set* h, hipStream_t s) {
+  if (h->forked) (void)hipStreamWaitEvent(s, h->ev_join, 0);
+  if (h->hc_active) {
+    const int32_t one = 1;
+    if (hipMemcpyAsync(h->d_hc_fail, &one, sizeof(one), hipMemcpyHostToDevice, s) == hipSuccess)
+      (void)gk_launch_hc_fallback(h->st, h->hc_x, h->hc_offs, h->d_long_list, h->d_long_n, h->d_hc_count,
+                                  h->d_hc_fail, s);
+    (void)hipStreamSynchronize(s);  // (`one` lives on this stack frame)
+  }
+  h->forked = false;
+  h->hc_active = false;
+}
+
 int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s) {
   hipEvent_t t0 = h->timing ? timing_event(h->tev_stats, h->n_stats) : nullptr;
   if (t0) HIP_TRY(hipEventRecord(t0, s));
@@ -606,7 +703,12 @@ int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s) {
   // records go to the host on the copy stream; the host walks the chains in
   // stats_join, while the GPU ingests.
   h->hc_active = false;
-  if (h->hc_min > 0) {
+  // (not while `s` is being captured into a graph: a replay would not hand
+  // the call to the worker; the device walks every chain then)
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (h->hc_min > 0 && s && hipStreamIsCapturing(s, &cap) != hipSuccess) cap = hipStreamCaptureStatusNone;
+  const bool hc_on = h->hc_min > 0 && cap == hipStreamCaptureStatusNone;
+  if (hc_on) {
     // (only the pick's count comes back here; the records follow in
     // run_host_chains when there are any -- every stream of the process
     // shares 4 hardware queues, and copies queued beside `aux` delayed it)
@@ -615,12 +717,14 @@ int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s) {
     HIP_TRY(hipMemcpyAsync(h->h_hc_count, h->d_hc_count, sizeof(int32_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipEventRecord(h->ev_hc, s));
     h->hc_x = x;
+    h->hc_offs = offs;
   }
   HIP_TRY(hipEventRecord(h->ev_fork, s));
   HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_fork, 0));
+  h->forked = true;
   HIP_TRY(gk_launch_stats_long(h->st, x, offs, h->d_long_list, h->d_long_n, h->d_long_count,
-                               h->hc_min > 0 ? h->d_hc_count : nullptr, h->aux));
-  h->hc_active = h->hc_min > 0;  // (stats_join walks the picked chains)
+                               hc_on ? h->d_hc_count : nullptr, h->aux));
+  h->hc_active = hc_on;  // (stats_join hands the picked chains to the worker)
   HIP_TRY(hipEventRecord(h->ev_join, h->aux));
   const bool presort = h->ps.list_ws && h->ps.ws && h->ps.ws_cap > 0;
   if (presort) {
@@ -637,20 +741,37 @@ int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s) {
 }
 
 int stats_join(gk_set* h, hipStream_t s, const GKQuery& q) {
-  int rc = GK_OK, taken = 0;
+  h->forked = false;
+  HIP_TRY(hipStreamWaitEvent(s, h->ev_join, 0));
   if (h->hc_active) {
     h->hc_active = false;
-    rc = run_host_chains(h, &taken);  // blocks this thread while the GPU ingests
-  }
-  HIP_TRY(hipStreamWaitEvent(s, h->ev_join, 0));
-  if (taken > 0) {
-    // (the next call's record readback is ordered after this copy: its fork
-    // waits on `s`)
-    HIP_TRY(hipMemcpyAsync(h->d_hc, h->h_hc, taken * sizeof(GKHostChainRec), hipMemcpyHostToDevice, s));
-    HIP_TRY(gk_launch_hc_apply(h->st, h->d_hc, h->d_hc_count, s));
+    // hand the call to the worker (it walks while the GPU ingests) and join
+    // it on `s`: nothing here waits on the host
+    if (!h->hc_thr.joinable()) {
+      h->hc_stop = false;
+      try {
+        h->hc_thr = std::thread(hc_worker_main, h);
+      } catch (...) {
+        return fail(GK_E_HIP, "cannot start the host-chain worker thread");
+      }
+    }
+    const uint64_t seq = ++h->hc_seq;
+    {
+      std::lock_guard<std::mutex> lk(h->hc_mu);
+      h->hc_jobs.push_back(seq);
+    }
+    h->hc_cv.notify_all();
+    HIP_TRY(gk_launch_hc_wait(h->h_hc_flag, seq, h->d_hc_fail, h->hc_timeout_s, s));
+    // (the copy engine reads the pinned records once k_hc_wait has seen the
+    // worker's flag; the next call's readback of them is ordered after it:
+    // its fork waits on `s`, and the next call first drains the worker)
+    HIP_TRY(hipMemcpyAsync(h->d_hc, h->h_hc, GK_HC_MAX * sizeof(GKHostChainRec), hipMemcpyHostToDevice, s));
+    HIP_TRY(gk_launch_hc_apply(h->st, h->d_hc, h->d_hc_count, h->d_hc_fail, s));
+    HIP_TRY(gk_launch_hc_fallback(h->st, h->hc_x, h->hc_offs, h->d_long_list, h->d_long_n, h->d_hc_count,
+                                  h->d_hc_fail, s));
   }
   HIP_TRY(gk_launch_query_list(h->st, h->d_long_list, h->d_long_count, q, s));
-  return rc;
+  return GK_OK;
 }
 
 // The ingest / flush launches of one call, with no host round trip: class 0
@@ -918,6 +1039,12 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
   okm &= hipMalloc(&h->d_hc_count, sizeof(int32_t)) == hipSuccess;
   okm &= hipHostMalloc(&h->h_hc, GK_HC_MAX * sizeof(GKHostChainRec)) == hipSuccess;
   okm &= hipHostMalloc(&h->h_hc_count, sizeof(int32_t)) == hipSuccess;
+  // the worker's flag: coherent pinned memory that k_hc_wait polls
+  okm &= hipHostMalloc(&h->h_hc_flag, sizeof(unsigned long long), hipHostMallocCoherent | hipHostMallocMapped) ==
+         hipSuccess;
+  okm &= hipMalloc(&h->d_hc_fail, sizeof(int32_t)) == hipSuccess;
+  if (h->h_hc_flag) *h->h_hc_flag = 0;
+  if (const char* e = getenv("GK_HC_FAIL")) h->hc_fail_inject = atoi(e) != 0;
   okm &= hipEventCreateWithFlags(&h->ev_hc, hipEventDisableTiming) == hipSuccess;
   if (h->P > 128 && !h->big[0]) {  // class 0 is a capacity-class kernel: presort long streams' batches
     okm &= hipMalloc(&h->ps.list_ws, S * sizeof(int64_t)) == hipSuccess;
@@ -951,6 +1078,7 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
 
 int gk_destroy(gk_set* h) {
   if (!h) return GK_OK;
+  hc_shutdown(h);  // the worker finishes its handed-out walks (their joins may be waiting on the device)
   (void)hipDeviceSynchronize();  // launches of this set may still be running on the caller's stream
   if (h->fold_scratch) gk_destroy(h->fold_scratch);
   GKState& st = h->st;
@@ -958,7 +1086,7 @@ int gk_destroy(gk_set* h) {
                   st.avg,     st.cls,        st.slot,        st.pbuf,        h->d_qs,
                   h->d_ctr,   h->d_zero_offs, h->d_long_list, h->d_long_n,
                   h->ps.list_ws, h->ps.list_b0, h->ps.ws,    h->ps.ws_need,  st.rtab,        st.n0,
-                  h->d_defer, h->d_hc,       h->d_hc_count};
+                  h->d_defer, h->d_hc,       h->d_hc_count,  h->d_hc_fail};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (int c = 0; c < GK_MAX_CLASSES; ++c)
@@ -977,7 +1105,7 @@ int gk_destroy(gk_set* h) {
   for (double* p : h->hc_buf) (void)hipHostFree(p);
   if (h->aux) (void)hipStreamDestroy(h->aux);
   for (void* p : {(void*)h->h_ws_need, (void*)h->h_ovf, (void*)h->h_ctr, (void*)h->h_qs, (void*)h->h_hc,
-                  (void*)h->h_hc_count})
+                  (void*)h->h_hc_count, (void*)h->h_hc_flag})
     if (p) (void)hipHostFree(p);
   delete h;
   return GK_OK;
@@ -1010,7 +1138,10 @@ int gk_ingest(gk_set* h, const double* values, const int64_t* offsets, void* str
   if (!rc) rc = begin_call(h, s);
   if (rc) return rc;
   rc = stats_fork(h, values, offsets, s);
-  if (rc) return rc;
+  if (rc) {
+    stats_abort(h, s);
+    return rc;
+  }
   rc = run_ingest(h, values, offsets, 0, s, GKQuery(), true);
   const int rj = stats_join(h, s, GKQuery());  // joined on every path
   const int rd = mark_done(h, s);
@@ -1121,7 +1252,10 @@ int gk_ingest_quantiles(gk_set* h, const double* values, const int64_t* offsets,
   if (!rc) rc = begin_call(h, s);
   if (rc) return rc;
   rc = stats_fork(h, values, offsets, s);
-  if (rc) return rc;
+  if (rc) {
+    stats_abort(h, s);
+    return rc;
+  }
   // add every value (gk:49-61), then quantiles() (gk:187-232): flush the
   // leftover pending values and answer from the LDS-resident table
   rc = run_ingest(h, values, offsets, 1, s, q, true);
@@ -1486,6 +1620,13 @@ int gk_flush_period(const gk_set* h) { return h ? h->P : -1; }
 int gk_capacity(const gk_set* h, int cls) {
   return (h && cls >= 0 && cls < h->st.nclass) ? h->st.cap[cls] : -1;
 }
+int64_t gk_host_chains_taken(gk_set* h) {
+  if (!h) return -1;
+  hc_drain(h);
+  std::lock_guard<std::mutex> lk(h->hc_mu);
+  return h->hc_last_rc == GK_OK ? h->hc_last_taken : 0;
+}
+
 int64_t gk_num_promoted(const gk_set* h) {
   if (!h) return -1;
   if (h->S == 0) return 0;

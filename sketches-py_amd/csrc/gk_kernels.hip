@@ -579,10 +579,34 @@ __global__ __launch_bounds__(256) void k_hc_prep(GKState st, const int64_t* __re
   if (t == 0) *hc_count = k;
 }
 
+// The join of an asynchronous host walk (round 4): one thread waits until the
+// set's host worker has published this call's sequence number in the pinned
+// flag word ((seq << 2) | 1 done / 2 failed; gk_capi.cpp hc_worker), with a
+// wall-clock bound (s_memrealtime, 100 MHz) after which the walk counts as
+// failed.  `fail` tells k_hc_apply / k_hc_fallback which of them applies the
+// picked streams' chains.  (Loads only: the flag is written by the host.)
+__global__ void k_hc_wait(const unsigned long long* __restrict__ flag, unsigned long long seq,
+                          int32_t* __restrict__ fail, unsigned long long timeout_ticks) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  int f = 1;
+  for (;;) {
+    const unsigned long long w = __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if ((w >> 2) >= seq) {
+      f = ((w >> 2) == seq && (w & 3) == 1) ? 0 : 1;
+      break;
+    }
+    if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) break;
+    __builtin_amdgcn_s_sleep(127);
+  }
+  *fail = f;
+}
+
 __global__ __launch_bounds__(256) void k_hc_apply(GKState st, const GKHostChainRec* __restrict__ recs,
-                                                  const int32_t* __restrict__ hc_count) {
+                                                  const int32_t* __restrict__ hc_count,
+                                                  const int32_t* __restrict__ fail) {
   const int t = threadIdx.x;
-  if (t >= *hc_count) return;
+  if ((fail && *fail) || t >= *hc_count) return;
   const GKHostChainRec r = recs[t];
   st.sum[r.s] = r.sum;
   st.avg[r.s] = r.avg;
@@ -800,6 +824,21 @@ __device__ __forceinline__ void stats_group_walk(const GKState& st, const double
       st.avg[s] = av;
     }
   }
+}
+
+// A failed host walk: the picked streams' chains on the device instead (the
+// one-wave-per-stream walk of k_stats_long), so their _sum/_avg/_min/_max are
+// exact either way.  Exits at once when the host walk succeeded.
+__global__ __launch_bounds__(64) void k_hc_fallback(GKState st, const double* __restrict__ x,
+                                                    const int64_t* __restrict__ offs,
+                                                    const int32_t* __restrict__ list,
+                                                    const int64_t* __restrict__ list_n,
+                                                    const int32_t* __restrict__ hc_count,
+                                                    const int32_t* __restrict__ fail) {
+  __shared__ double2 buf[64];
+  if (*fail == 0) return;
+  const int k = *hc_count;
+  for (int w = blockIdx.x; w < k; w += gridDim.x) stats_long_bcast(st, x, offs, list, list_n, w, threadIdx.x, buf);
 }
 
 __global__ __launch_bounds__(64) void k_stats_long(GKState st, const double* __restrict__ x,
@@ -1945,6 +1984,16 @@ __global__ __launch_bounds__(64) void k_ingest_big(GKState st, const double* __r
 //    prefix(g) + d - 1, one ballot + popcount per entry slot and quantile.
 // ===========================================================================
 #define SMALL_CAP GK_SMALL_CAP
+// entry (g, d) of the LDS table packed in 32 bits (1) or as two int32 (0)
+#ifndef GK_GD16
+#define GK_GD16 1
+#endif
+#ifndef GK_DPP64
+#define GK_DPP64 1  // register sort: 64-bit DPP partner moves
+#endif
+#ifndef GK_TPRED
+#define GK_TPRED 1  // T and its divider made one flush ahead
+#endif
 #ifndef GK_SMALL_WAVES
 #define GK_SMALL_WAVES 6  // min waves per SIMD asked of the register allocator
 #endif
@@ -2022,7 +2071,15 @@ struct SmallLDS {
   // as ds_read2_b64 immediates
   alignas(16) double mv[64 * VPL + 64 + 2];  // values grouped by gap, +inf after the last; [last] trash
   alignas(16) double tv[SMALL_TVN];        // entry values at pidx(i); +inf from E up to E+63 (<= 127)
+#if GK_GD16
+  // entry (g, d) at i packed in one word (g low 16 bits, d high 16 bits,
+  // both unsigned: the stream's load checks g, d >= 0 and g + d <= 65535,
+  // which every flush of the add path keeps while T <= 65535, DESIGN.md
+  // §5); [j0+2] read as successor; [129] trash
+  alignas(16) uint32_t tgd[SMALL_CAP + 4];
+#else
   alignas(16) int2 tgd[SMALL_CAP + 2];     // entry (g, d) at i; [j0+2] read as successor; [129] trash
+#endif
   union {
     // per gap (padded index): first the member count (.x, the count atomics),
     // then the record (m<<24 | k<<16 | member base<<8 | out base, G+d-1)
@@ -2091,14 +2148,25 @@ __device__ __forceinline__ CsDiv make_csdiv(int T) {
   return c;
 }
 
+#if GK_GD16
+// (g, d) <-> the packed LDS word: g in bits 0-15, d in bits 16-31 (one v_perm_b32)
+__device__ __forceinline__ uint32_t gd_pack(int g, int d) { return __builtin_amdgcn_perm((uint32_t)d, (uint32_t)g, 0x05040100u); }
+__device__ __forceinline__ int gd_g(uint32_t w) { return (int)(w & 0xffffu); }
+__device__ __forceinline__ int gd_d(uint32_t w) { return (int)(w >> 16); }
+#endif
+
 template <int VPL, int DUPG = -1>
 __device__ __forceinline__ void small_put(SmallLDS<VPL>& L, int pos, double v, int g, int d) {
   L.tv[pidx(pos)] = v;
+#if GK_GD16
+  L.tgd[pos] = gd_pack(g, d);
+#else
   L.tgd[pos] = make_int2(g, d);
   if constexpr (DUPG >= 0 && GK_DUPG(DUPG)) {
     dup_st(&L.tv[pidx(pos)], v);
     dup_st(&L.tgd[pos], make_int2(g, d));
   }
+#endif
 }
 
 // gi[gap].x = m << 24 | k << 16 | member base << 8 | out base (m, k <= 128)
@@ -2144,7 +2212,25 @@ __device__ __forceinline__ int lane_xor_i32(int v, int lane) {
 
 template <int J>
 __device__ __forceinline__ double lane_xor_f64(double v, int lane) {
-  return __hiloint2double(lane_xor_i32<J>(__double2hiint(v), lane), lane_xor_i32<J>(__double2loint(v), lane));
+  // pure DPP partners as one 64-bit DPP move: both halves land in a register
+  // pair (per 32-bit half the compiler copied one half into the pair: an
+  // extra v_mov per compare-exchange)
+  if constexpr (!GK_DPP64)
+    return __hiloint2double(lane_xor_i32<J>(__double2hiint(v), lane), lane_xor_i32<J>(__double2loint(v), lane));
+  else if constexpr (J == 1) return __builtin_amdgcn_mov_dpp(v, GK_DPP_QPERM(1, 0, 3, 2), 0xf, 0xf, true);
+  else if constexpr (J == 2) return __builtin_amdgcn_mov_dpp(v, GK_DPP_QPERM(2, 3, 0, 1), 0xf, 0xf, true);
+  else if constexpr (J == 3) return __builtin_amdgcn_mov_dpp(v, GK_DPP_QPERM(3, 2, 1, 0), 0xf, 0xf, true);
+  else if constexpr (J == 7) return __builtin_amdgcn_mov_dpp(v, GK_DPP_ROW_HALF_MIRROR, 0xf, 0xf, true);
+  else if constexpr (J == 15) return __builtin_amdgcn_mov_dpp(v, GK_DPP_ROW_MIRROR, 0xf, 0xf, true);
+  else if constexpr (J == 8) return __builtin_amdgcn_mov_dpp(v, GK_DPP_ROW_ROR8, 0xf, 0xf, true);
+  else if constexpr (J == 4)
+    return __builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp(v, GK_DPP_ROW_HALF_MIRROR, 0xf, 0xf, true),
+                                    GK_DPP_QPERM(3, 2, 1, 0), 0xf, 0xf, true);
+  else if constexpr (J == 31) {
+    const double m = __builtin_amdgcn_mov_dpp(v, GK_DPP_ROW_MIRROR, 0xf, 0xf, true);
+    return __hiloint2double(gk_xor16(__double2hiint(m), lane), gk_xor16(__double2loint(m), lane));
+  } else
+    return __hiloint2double(lane_xor_i32<J>(__double2hiint(v), lane), lane_xor_i32<J>(__double2loint(v), lane));
 }
 
 // a[r] against the value at lane ^ X (same r); the lower lane (bit LB of the
@@ -2194,11 +2280,11 @@ __device__ __forceinline__ void sort128_2(double (&a)[2], int lane) {
 // untouched... except for the counts, which the caller discards).
 template <int VPL, int K, typename AfterSearch>
 __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const double (&xv)[VPL], const int cnt,
-                                           const int T, const int lane, AfterSearch&& after_search) {
+                                           const int T, const CsDiv cd, const int lane, AfterSearch&& after_search) {
   static_assert(K == 2, "the 128-entry class holds 2 entries per lane");
-  // the chunk-size divider first: its magic-number load (a scalar load)
-  // returns during the gap search instead of stalling after the scan
-  const CsDiv cd = make_csdiv(T);
+  // cd = make_csdiv(T): the chunk-size divider, made by the caller (for an
+  // automatic flush one flush ahead, so that its magic-number scalar load is
+  // not waited for on the flush's critical path)
   if constexpr (VPL == 2) {
     // ---- empty table (every stream's first flush): all values are tail
     //      (gk:85-92), so the flush is a sort and a cut into chunks of
@@ -2279,11 +2365,21 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
   int eg[K + 1], ed[K + 1], em[K];
   {
     int2 gd[K + 1];
+#if GK_GD16
+    {
+      const uint2 a = *(const uint2*)&L.tgd[j0];
+      const uint32_t a2 = L.tgd[j0 + 2];
+      gd[0] = make_int2(gd_g(a.x), gd_d(a.x));
+      gd[1] = make_int2(gd_g(a.y), gd_d(a.y));
+      gd[2] = make_int2(gd_g(a2), gd_d(a2));
+    }
+#else
     const int4 a = *(const int4*)&L.tgd[j0];
     gd[0] = make_int2(a.x, a.y);
     gd[1] = make_int2(a.z, a.w);
     gd[2] = L.tgd[j0 + 2];
-    if constexpr (GK_DUPG(4)) {
+#endif
+    if constexpr (!GK_GD16 && GK_DUPG(4)) {
       dup_ld((const int4*)&L.tgd[j0]);
       dup_ld(&L.tgd[j0 + 2]);
       dup_ld(&L.tv[pj0]);
@@ -2638,7 +2734,12 @@ __device__ __forceinline__ int small_rank_count(SmallLDS<VPL>& L, int E, int64_t
   const int j0 = 2 * lane;
   I run[2];
   {
+#if GK_GD16
+    const uint2 w = *(const uint2*)&L.tgd[j0];
+    const int4 gd = make_int4(gd_g(w.x), gd_d(w.x), gd_g(w.y), gd_d(w.y));
+#else
     const int4 gd = *(const int4*)&L.tgd[j0];
+#endif
     const int g0 = (j0 < E) ? gd.x : 0, g1 = (j0 + 1 < E) ? gd.z : 0;
     const I lsum = (I)g0 + (I)g1;
     I bex;
@@ -2929,12 +3030,26 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
 #pragma unroll
       for (int r = 0; r < SMALL_CAP / 64; ++r)
         rc[r] = (lane + 64 * r < E) ? t4[lane + 64 * r] : make_int4(0, 0, 0, 0);
+#if GK_GD16
+      // packed (g, d): every entry needs g, d >= 0 and g + d <= 65535, and
+      // the call's largest T must stay <= 65535 (then every flush keeps
+      // g + d <= 65535: DESIGN.md §5); else the stream takes the next class
+      bool bad = (double)(n + (Lx > 0 ? Lx : 0) - 1) * st.two_eps >= 65535.0;
+#pragma unroll
+      for (int r = 0; r < SMALL_CAP / 64; ++r)
+        bad |= (lane + 64 * r < E) && ((rc[r].z | rc[r].w) < 0 || rc[r].z + rc[r].w > 65535);
+      ok = __builtin_amdgcn_ballot_w64(bad) == 0;
+#endif
 #pragma unroll
       for (int r = 0; r < SMALL_CAP / 64; ++r) {
         const int j = lane + 64 * r;
         if (j < E) {
           L.tv[pidx(j)] = __hiloint2double(rc[r].y, rc[r].x);
+#if GK_GD16
+          L.tgd[j] = gd_pack(rc[r].z, rc[r].w);
+#else
           L.tgd[j] = make_int2(rc[r].z, rc[r].w);
+#endif
         }
       }
       small_pad(L.tv, E, lane);
@@ -2952,6 +3067,8 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
     // a multiply and a truncation (n >= 1 at every flush, and gk_count_ok
     // above bounds T by GK_T_CLAMP for the whole call: no clamps)
     double nm1 = (double)(n - 1);
+    int Tpred = -1;  // T and divider of the next automatic flush (made one flush ahead)
+    CsDiv cdpred = {1, 1u << 23};
     double xv[VPL];
 #pragma unroll
     for (int r = 0; r < VPL; ++r) xv[r] = 0.0;
@@ -2981,14 +3098,26 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
       };
       n += nadd;
       nm1 += (double)(int)nadd;
-      const int T = __builtin_amdgcn_readfirstlane((int)(st.two_eps * nm1));
+      // T of an automatic flush of P adds (every flush but a call's first
+      // and its final partial one) and its divider were made one flush ahead
+      int T;
+      CsDiv cd;
+      if (GK_TPRED && nadd == P && Tpred >= 0) {
+        T = Tpred;
+        cd = cdpred;
+      } else {
+        T = __builtin_amdgcn_readfirstlane((int)(st.two_eps * nm1));
+        cd = make_csdiv(T);
+      }
+      Tpred = __builtin_amdgcn_readfirstlane((int)(st.two_eps * (nm1 + (double)P)));
+      cdpred = make_csdiv(Tpred);
       GK_MARK(L, 8);
       int nE;
       if constexpr (SMALL_CAP > 128)
-        nE = E <= 127 ? flush_small<VPL, 2>(L, E, xv, cnt, T, lane, prefetch)
-                      : flush_small<VPL, 4>(L, E, xv, cnt, T, lane, prefetch);
+        nE = E <= 127 ? flush_small<VPL, 2>(L, E, xv, cnt, T, cd, lane, prefetch)
+                      : flush_small<VPL, 4>(L, E, xv, cnt, T, cd, lane, prefetch);
       else
-        nE = flush_small<VPL, 2>(L, E, xv, cnt, T, lane, prefetch);
+        nE = flush_small<VPL, 2>(L, E, xv, cnt, T, cd, lane, prefetch);
       if (nE < 0) {
         ok = false;
         break;
@@ -3042,7 +3171,12 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
 #pragma unroll
       for (int r = 0; r < 2; ++r) {
         v[r] = L.tv[pidx(lane + 64 * r)];
+#if GK_GD16
+        const uint32_t w = L.tgd[lane + 64 * r];
+        gd[r] = make_int2(gd_g(w), gd_d(w));
+#else
         gd[r] = L.tgd[lane + 64 * r];
+#endif
       }
 #pragma unroll
       for (int r = 0; r < 2; ++r)
@@ -3820,9 +3954,25 @@ hipError_t gk_launch_hc_prep(const GKState& st, const int64_t* offs, const int32
 }
 
 hipError_t gk_launch_hc_apply(const GKState& st, const GKHostChainRec* recs, const int32_t* hc_count,
-                              hipStream_t stream) {
+                              const int32_t* fail, hipStream_t stream) {
   if (st.S <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_hc_apply, dim3(1), dim3(GK_HC_MAX), 0, stream, st, recs, hc_count);
+  hipLaunchKernelGGL(k_hc_apply, dim3(1), dim3(GK_HC_MAX), 0, stream, st, recs, hc_count, fail);
+  return hipGetLastError();
+}
+
+hipError_t gk_launch_hc_wait(const unsigned long long* flag, unsigned long long seq, int32_t* fail,
+                             double timeout_s, hipStream_t stream) {
+  hipLaunchKernelGGL(k_hc_wait, dim3(1), dim3(64), 0, stream, flag, seq, fail,
+                     (unsigned long long)(timeout_s * 1e8));
+  return hipGetLastError();
+}
+
+hipError_t gk_launch_hc_fallback(const GKState& st, const double* x, const int64_t* offs, const int32_t* long_list,
+                                 const int64_t* long_n, const int32_t* hc_count, const int32_t* fail,
+                                 hipStream_t stream) {
+  if (st.S <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_hc_fallback, dim3(GK_HC_MAX), dim3(64), 0, stream, st, x, offs, long_list, long_n, hc_count,
+                     fail);
   return hipGetLastError();
 }
 

@@ -116,8 +116,17 @@ struct GKHostChainRec {
 hipError_t gk_launch_hc_prep(const GKState& st, const int64_t* offs, const int32_t* long_list, const int64_t* long_n,
                              const int32_t* long_count, int64_t min_len, int rel_pct, int64_t budget_factor,
                              GKHostChainRec* recs, int32_t* hc_count, hipStream_t stream);
+// fail (device, may be NULL): set by gk_launch_hc_wait; nonzero = the host
+// walk failed and gk_launch_hc_fallback walks the picked streams instead
 hipError_t gk_launch_hc_apply(const GKState& st, const GKHostChainRec* recs, const int32_t* hc_count,
-                              hipStream_t stream);
+                              const int32_t* fail, hipStream_t stream);
+// waits (one thread, s_sleep) until *flag >> 2 >= seq, at most timeout_s
+// seconds; *fail = 0 iff the flag is (seq << 2) | 1
+hipError_t gk_launch_hc_wait(const unsigned long long* flag, unsigned long long seq, int32_t* fail,
+                             double timeout_s, hipStream_t stream);
+hipError_t gk_launch_hc_fallback(const GKState& st, const double* x, const int64_t* offs, const int32_t* long_list,
+                                 const int64_t* long_n, const int32_t* hc_count, const int32_t* fail,
+                                 hipStream_t stream);
 // quantiles of the listed streams from their committed tables (after the join)
 hipError_t gk_launch_query_list(const GKState& st, const int32_t* list, const int32_t* count, const GKQuery& q,
                                 hipStream_t stream);

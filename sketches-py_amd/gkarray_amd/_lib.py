@@ -76,6 +76,7 @@ SYMBOLS = {
     "gk_flush_period": (_INT, [_P]),
     "gk_capacity": (_INT, [_P, _INT]),
     "gk_num_promoted": (_I64, [_P]),
+    "gk_host_chains_taken": (_I64, [_P]),
     "gk_timing_enable": (_INT, [_P, _INT]),
     "gk_timing_read": (_INT, [_P, ctypes.POINTER(_D), ctypes.POINTER(_D), ctypes.POINTER(_I64)]),
 }
@@ -126,8 +127,16 @@ def load(path=None):
         handle = ctypes.CDLL(p)
     except OSError as e:  # pragma: no cover - depends on the ROCm install
         raise GKBackendError(GK_E_HIP, "cannot load %s: %s" % (p, e))
+    override = path is None and bool(os.environ.get("GK_LIB_PATH"))
     for name, (res, args) in SYMBOLS.items():
-        fn = getattr(handle, name)
+        try:
+            fn = getattr(handle, name)
+        except AttributeError:
+            if not override:
+                raise
+            # an older build under A/B (GK_LIB_PATH): entry points it predates stay unbound
+            sys.stderr.write("gkarray_amd: %s lacks %s\n" % (p, name))
+            continue
         fn.restype = res
         fn.argtypes = args
     if path is None:

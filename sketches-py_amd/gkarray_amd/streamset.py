@@ -114,6 +114,12 @@ class StreamSet:
     def num_promoted(self):
         return self._lib.gk_num_promoted(self._h)
 
+    @property
+    def host_chains_taken(self):
+        """Streams whose _sum/_avg chains the host walked in the last
+        completed ingest (diagnostics; waits for the set's host worker)."""
+        return self._lib.gk_host_chains_taken(self._h)
+
     def _sp(self):
         return _stream_ptr(self.device)
 

@@ -67,6 +67,40 @@ def same_float(a, b):
     return a.tobytes() == b.tobytes()
 
 
+def zero_sign_unpinned(vals, n, eps, q):
+    """True iff the reference's answer to q is a zero whose SIGN is not a
+    function of the input: the small-n branch (n < 1/eps, gk:169-171 /
+    gk:200-202) calls numpy.percentile on the table values, and numpy's
+    partition (introselect, or x86-simd-sort's AVX-512 / AVX2 network on
+    machines that have them -- CPU-dependent) may place -0.0 or +0.0 at the
+    two interpolation positions.  numpy 2.2.6's _lerp returns -0.0 only in its
+    gamma >= 0.5 branch with BOTH positions -0.0 (b - (b-a)(1-g) = -0 - +0);
+    so the sign is open exactly when: gamma >= 0.5, prev < E-1, the stable-
+    ordered values at prev and prev+1 are both zeros, and the table holds
+    both +0.0 and -0.0.  Everywhere else the answer is pinned bit for bit
+    (tests/test_oracle_golden.py::test_zero_sign_class_is_exact fuzzes the
+    claim against numpy itself).  `vals`: the table values in table order."""
+    if not (float(n) < 1.0 / eps) or not (0.0 <= q <= 1.0):
+        return False
+    E = len(vals)
+    if E < 2:
+        return False
+    vi = float(E - 1) * ((q * 100) / 100.0)
+    if vi >= E - 1 or vi < 0:
+        return False
+    prev = int(np.floor(vi))
+    if vi - prev < 0.5 or vals[prev] != 0 or vals[prev + 1] != 0:
+        return False
+    zs = [bool(np.signbit(v)) for v in vals if v == 0]
+    return any(zs) and not all(zs)
+
+
+def unpinned_mask(table, n, eps, qs):
+    """zero_sign_unpinned for each q of qs; `table`: list of (v, g, d)."""
+    vals = [float(t[0]) for t in table]
+    return [zero_sign_unpinned(vals, n, eps, float(q)) for q in qs]
+
+
 def same_table(t1, t2):
     if len(t1) != len(t2):
         return False

@@ -11,7 +11,7 @@ import torch
 import golden_io as G
 from gk_oracle_c import OracleSet
 from parity_util import (_ss, assert_same_quantiles, assert_same_state, assert_same_tables, csr, gen, ingest_np,
-                         small_n, small_of)
+                         golden_mask, small_of)
 
 CPU = "cpu"
 
@@ -32,18 +32,18 @@ def test_golden_streams_cpu():
                                   G.get(c["id"], "pending").view(np.int64)), c
             got = [st["n"][k], st["min"][k], st["max"][k], st["sum"][k], st["avg"][k]]
             assert all(G.same_float(a, b) for a, b in zip(got, G.get(c["id"], "stats_before_query"))), c
-        sm = small_n(st["n"], eps)
+        um = lambda k, c, qs: golden_mask(G.tables(c["id"], "final")[0], st["n"][k], eps, qs)  # noqa: E731
         q = ss.quantiles(G.index()["qs"], single=True).numpy()
         for k, c in enumerate(cs):
-            assert_same_quantiles(q[k], G.get(c["id"], "q_single"), "quantile %r" % c, sm[k])
+            assert_same_quantiles(q[k], G.get(c["id"], "q_single"), "quantile %r" % c, um(k, c, G.index()["qs"]))
             assert G.same_table(ss.table(k), G.tables(c["id"], "final")[0]), c
         q = ss.quantiles(G.index()["qs"]).numpy()
         q2 = ss.quantiles(G.index()["qs_unsorted"]).numpy()
         q3 = ss.quantiles(G.index()["qs_oor"]).numpy()
         for k, c in enumerate(cs):
-            assert_same_quantiles(q[k], G.get(c["id"], "q_sorted"), "quantiles %r" % c, sm[k])
-            assert_same_quantiles(q2[k], G.get(c["id"], "q_unsorted"), "unsorted %r" % c, sm[k])
-            assert_same_quantiles(q3[k], G.get(c["id"], "q_oor"), "oor %r" % c, sm[k])
+            assert_same_quantiles(q[k], G.get(c["id"], "q_sorted"), "quantiles %r" % c, um(k, c, G.index()["qs"]))
+            assert_same_quantiles(q2[k], G.get(c["id"], "q_unsorted"), "unsorted %r" % c, um(k, c, G.index()["qs_unsorted"]))
+            assert_same_quantiles(q3[k], G.get(c["id"], "q_oor"), "oor %r" % c, um(k, c, G.index()["qs_oor"]))
 
 
 def test_per_flush_golden_snapshots_cpu():
@@ -81,7 +81,7 @@ def test_golden_merges_and_query_mid_cpu():
         got = [st["n"][0], st["min"][0], st["max"][0], st["sum"][0], st["avg"][0]]
         assert all(G.same_float(a, b) for a, b in zip(got, G.get(cid, "merged_stats"))), c
         assert_same_quantiles(sets[0].quantiles(G.index()["qs"]).numpy()[0], G.get(cid, "merged_q"), c,
-                              small_n(st["n"][0], eps))
+                              golden_mask(steps[-1], st["n"][0], eps, G.index()["qs"]))
     for c in G.cases("query_mid"):
         cid, eps = c["id"], c["eps"]
         xs = G.get(cid, "x")
@@ -91,7 +91,7 @@ def test_golden_merges_and_query_mid_cpu():
         for k, p in enumerate(pts):
             ingest_np(ss, [xs[prev:p]])
             assert_same_quantiles(ss.quantiles([0.1, 0.5, 0.9]).numpy()[0], G.get(cid, "mid_q")[k], c,
-                                  small_n(p, eps))
+                                  golden_mask(G.tables(cid, "mid_tables")[k], p, eps, [0.1, 0.5, 0.9]))
             prev = p
 
 

@@ -9,7 +9,15 @@ the path switched off (GK_HOST_CHAINS=0), across two calls (the second
 starts from a non-trivial pre-call state), with signed zeros, infinities and
 a NaN in the host-walked streams, and with a fused quantile query (answered
 for the long streams after the host results are applied).
+
+Round 4: the host walk is asynchronous (a worker thread of the set, joined on
+the caller's stream by k_hc_wait): gk_ingest returns before the ingest kernel
+completes; the number of streams the host took is asserted; a
+failed host walk (GK_HC_FAIL=1 injects one) is walked on the device instead
+(k_hc_fallback), with the same bits.
 """
+import time
+
 import numpy as np
 import pytest
 import torch
@@ -52,6 +60,7 @@ def run(dev, monkeypatch, env):
         x = torch.from_numpy(np.concatenate(seqs)).to(dev)
         q = ss.ingest(x, torch.from_numpy(offs).to(dev), quantiles=QS).cpu().numpy()
         st = {k: t.cpu().numpy() for k, t in ss.stats().items()}
+        st["taken"] = ss.host_chains_taken
         out.append((seqs, offs, q, st))
     return out
 
@@ -66,6 +75,8 @@ def test_host_chains_match_oracle_and_device_path(gpu_device, monkeypatch, threa
     dev = run(gpu_device, monkeypatch, {"GK_HOST_CHAINS": "0"})
     o = OracleSet(300, 0.001)
     for (seqs, offs, q, st), (_, _, qd, std) in zip(host, dev):
+        assert st["taken"] > 0, "the host walked no chain"
+        assert std["taken"] == 0
         o.ingest(np.concatenate(seqs), offs)
         ost = o.stats()
         for k in STATS:
@@ -84,7 +95,63 @@ def test_host_chains_take_only_the_longest(gpu_device, monkeypatch):
     host = run(gpu_device, monkeypatch, {"GK_HOST_CHAIN_MIN": "20000", "GK_HOST_CHAIN_THREADS": "1"})
     o = OracleSet(300, 0.001)
     for seqs, offs, q, st in host:
+        assert 0 < st["taken"] < 24, st["taken"]  # 24 long streams, budget 4 x the longest
         o.ingest(np.concatenate(seqs), offs)
         ost = o.stats()
         for k in STATS:
             assert np.array_equal(bits(st[k]), bits(ost[k])), k
+
+
+def test_failed_host_walk_is_walked_on_the_device(gpu_device, monkeypatch):
+    """GK_HC_FAIL=1: the worker reports a failure after its walk; k_hc_wait
+    sees status 2, k_hc_apply skips the records and k_hc_fallback walks the
+    picked streams on the device -- same bits as the oracle and as the device
+    path, and no error surfaces (the set is not broken)."""
+    bad = run(gpu_device, monkeypatch, {"GK_HOST_CHAIN_MIN": "50000", "GK_HOST_CHAIN_THREADS": "2",
+                                        "GK_HC_FAIL": "1"})
+    monkeypatch.delenv("GK_HC_FAIL")
+    dev = run(gpu_device, monkeypatch, {"GK_HOST_CHAINS": "0"})
+    o = OracleSet(300, 0.001)
+    for (seqs, offs, q, st), (_, _, qd, std) in zip(bad, dev):
+        assert st["taken"] == 0
+        o.ingest(np.concatenate(seqs), offs)
+        ost = o.stats()
+        for k in STATS:
+            assert np.array_equal(bits(st[k]), bits(ost[k])), "fallback vs oracle: %s" % k
+            assert np.array_equal(bits(st[k]), bits(std[k])), "fallback vs device chains: %s" % k
+        assert np.array_equal(bits(q), bits(qd)), "quantiles: fallback vs device chains"
+
+
+def test_ingest_with_host_chains_returns_before_the_kernel(gpu_device, monkeypatch):
+    """with a stream past the host-chain threshold (2^20
+    values, the default) in the batch, gk_ingest_quantiles only enqueues --
+    it returns while the ingest is still running on the device -- and the
+    joined results are exact."""
+    monkeypatch.delenv("GK_HOST_CHAIN_MIN", raising=False)
+    monkeypatch.delenv("GK_HOST_CHAINS", raising=False)
+    rng = np.random.default_rng(77)
+    lens = rng.integers(1, 2000, 64)
+    lens[0] = 3 << 20
+    seqs = [rng.lognormal(0.0, 1.0, int(L)) for L in lens]
+    offs = np.zeros(65, np.int64)
+    offs[1:] = np.cumsum(lens)
+    x = torch.from_numpy(np.concatenate(seqs)).to(gpu_device)
+    o_t = torch.from_numpy(offs).to(gpu_device)
+    ss = _ss(64, 0.001, gpu_device)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    q = ss.ingest(x, o_t, quantiles=QS, sync=False)
+    dt = time.perf_counter() - t0
+    busy = not torch.cuda.current_stream(gpu_device).query()
+    ss.sync()
+    total = time.perf_counter() - t0
+    assert busy, "the call returned after the device work had finished (%.1f ms, total %.1f ms)" % (
+        dt * 1e3, total * 1e3)
+    assert ss.host_chains_taken == 1
+    o = OracleSet(64, 0.001)
+    o.ingest(np.concatenate(seqs), offs)
+    ost = o.stats()
+    st = {k: t.cpu().numpy() for k, t in ss.stats().items()}
+    for k in STATS:
+        assert np.array_equal(bits(st[k]), bits(ost[k])), k
+    assert_same_quantiles(q.cpu().numpy(), o.quantiles(QS), "fused quantiles", small_of(o, 0.001))
