@@ -163,6 +163,8 @@ struct gk_set {
   // streams' chains (k_stats on the caller's stream); the ingest waits for it
   hipStream_t aux2 = nullptr;
   hipEvent_t ev_presort = nullptr;
+  hipEvent_t ev_wg = nullptr;  // k_ingest_wg (on aux2, after the presort) done
+  bool wg_trace = false;       // GK_WG_TRACE=1 at creation: its stream count per completed call on stderr (tests)
   std::vector<hipStream_t> hc_streams;
   std::vector<double*> hc_buf;
   std::vector<hipEvent_t> hc_ev;
@@ -277,6 +279,8 @@ void poll(gk_set* h, bool block) {
     return;
   }
   h->done_pending = false;
+  if (h->ps.wg_count && h->wg_trace && h->h_ctr[GK_CTR_WORDS] > 0)
+    fprintf(stderr, "[gk] k_ingest_wg: %d stream(s)\n", h->h_ctr[GK_CTR_WORDS]);
   const int32_t fatal = h->h_ctr[GK_CTR_FATAL];
   if (fatal > h->fatal_seen && h->sticky == GK_OK) {
     char buf[256];
@@ -437,6 +441,8 @@ int take_sticky(gk_set* h) {
 // End of a call's device work on `s`: counters -> pinned host memory.
 int mark_done(gk_set* h, hipStream_t s) {
   HIP_TRY(hipMemcpyAsync(h->h_ctr, h->d_ctr, GK_CTR_WORDS * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  if (h->ps.wg_count && h->wg_trace)
+    HIP_TRY(hipMemcpyAsync(h->h_ctr + GK_CTR_WORDS, h->ps.wg_count, sizeof(int32_t), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipEventRecord(h->ev_done, s));
   h->done_pending = true;
   return GK_OK;
@@ -473,7 +479,7 @@ bool stats_fused(const gk_set* h);
 // whose length is *count_ptr (device).  Overflowing streams go to round r's list.
 hipError_t launch_class(gk_set* h, int c, const double* x, const int64_t* offs, const int32_t* list,
                         const int32_t* count_ptr, int r, int force, const GKQuery& q, hipStream_t stream,
-                        bool prio = false) {
+                        bool prio = false, bool wg = false) {
   if (c > 0 && h->st.alloc[c] == 0) return hipSuccess;  // no slot yet: no member
   unsigned long long* work = work_counter(h, c == 0 && h->st.cap[0] == GK_SMALL_CAP && !h->big[0]);
   if (!work) return hipErrorInvalidValue;
@@ -485,6 +491,7 @@ hipError_t launch_class(gk_set* h, int c, const double* x, const int64_t* offs, 
                           h->d_ws[c], h->ws_bytes[c], h->ws_blocks[c], ovf_count(h, r), ovf_list(h, r), q, work,
                           prio ? h->d_long_list : nullptr, prio ? h->d_long_count : nullptr,
                           prio && h->ps.ws ? h->ps.ws : nullptr, prio && h->ps.ws ? h->ps.list_ws : nullptr,
+                          prio && wg ? h->ps.wg_count : nullptr,
                           (prio && c == 0 && stats_fused(h)) ? h->fused_stats : 0, stream);
 }
 
@@ -820,9 +827,21 @@ int run_ingest(gk_set* h, const double* x, const int64_t* offs, int force, hipSt
   const bool timed = h->timing && x != nullptr;
   hipEvent_t t0 = timed ? timing_event(h->tev_flush, h->n_flush) : nullptr;
   if (t0) HIP_TRY(hipEventRecord(t0, stream));
-  HIP_TRY(launch_class(h, 0, x, offs, nullptr, nullptr, 0, force, q, stream, prio && x != nullptr));
+  // the longest presorted streams of an ingest: one workgroup each, on aux2
+  // right behind their presort, beside the class-0 launch (which skips them)
+  const bool wg = prio && x != nullptr && h->ps.wg_count && h->aux2 && h->ps.list_ws && h->ps.ws && h->ps.ws_cap > 0;
+  if (wg) {
+    unsigned long long* wwork = work_counter(h, false);
+    if (!wwork) return fail(GK_E_HIP, "no hand-out counter left for k_ingest_wg");
+    HIP_TRY(gk_launch_ingest_wg(h->st, x, offs, h->d_long_list, h->ps.wg_count, 0, force, ovf_count(h, 0),
+                                ovf_list(h, 0), wwork, h->ps, h->aux2));
+    HIP_TRY(hipEventRecord(h->ev_wg, h->aux2));
+  }
+  HIP_TRY(launch_class(h, 0, x, offs, nullptr, nullptr, 0, force, q, stream, prio && x != nullptr, wg));
   hipEvent_t t1 = timed ? timing_event(h->tev_flush, h->n_flush) : nullptr;
   if (t1) HIP_TRY(hipEventRecord(t1, stream));
+  // (its overflow entries feed the promotion rounds below)
+  if (wg) HIP_TRY(hipStreamWaitEvent(stream, h->ev_wg, 0));
   if (!h->no_members)
     for (int c = 1; c < R; ++c)
       HIP_TRY(launch_class(h, c, x, offs, h->d_list[c], h->d_ctr + GK_CTR_LCNT + c, 0, force, q, stream));
@@ -1004,7 +1023,7 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
     h->d_long_count = h->d_ctr + GK_CTR_LONG;
     h->d_work = (unsigned long long*)((char*)h->d_ctr + GK_CALL_WORK);
   }
-  okm &= hipHostMalloc(&h->h_ctr, GK_CTR_WORDS * sizeof(int32_t)) == hipSuccess;
+  okm &= hipHostMalloc(&h->h_ctr, (GK_CTR_WORDS + 1) * sizeof(int32_t)) == hipSuccess;  // + the call's wg count
   okm &= hipMalloc(&h->d_defer, S * sizeof(int32_t)) == hipSuccess;
   if (h->h_ctr) memset(h->h_ctr, 0, GK_CTR_WORDS * sizeof(int32_t));
   okm &= hipEventCreateWithFlags(&h->ev_done, hipEventDisableTiming) == hipSuccess;
@@ -1052,6 +1071,13 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
     okm &= hipMalloc(&h->ps.ws_need, sizeof(int64_t)) == hipSuccess;
     okm &= hipHostMalloc(&h->h_ws_need, sizeof(int64_t)) == hipSuccess;
     if (h->h_ws_need) *h->h_ws_need = 0;
+    // the longest presorted streams: one workgroup each (k_ingest_wg, 2048
+    // class, P <= 1024; GK_WG=0 turns it off); their count is a per-call word
+    bool wg = st.cap[0] == 2048 && h->P <= 1024;
+    if (const char* e = getenv("GK_WG")) wg = wg && atoi(e) != 0;
+    if (wg) h->ps.wg_count = h->d_ctr + GK_CTR_WG;
+    h->wg_trace = getenv("GK_WG_TRACE") != nullptr;
+    okm &= hipEventCreateWithFlags(&h->ev_wg, hipEventDisableTiming) == hipSuccess;
   }
   if (!okm) {
     gk_destroy(h);
@@ -1102,6 +1128,7 @@ int gk_destroy(gk_set* h) {
   if (h->hc_copy) (void)hipStreamDestroy(h->hc_copy);
   if (h->aux2) (void)hipStreamDestroy(h->aux2);
   if (h->ev_presort) (void)hipEventDestroy(h->ev_presort);
+  if (h->ev_wg) (void)hipEventDestroy(h->ev_wg);
   for (double* p : h->hc_buf) (void)hipHostFree(p);
   if (h->aux) (void)hipStreamDestroy(h->aux);
   for (void* p : {(void*)h->h_ws_need, (void*)h->h_ovf, (void*)h->h_ctr, (void*)h->h_qs, (void*)h->h_hc,

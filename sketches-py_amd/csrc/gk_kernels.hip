@@ -320,6 +320,16 @@ __global__ __launch_bounds__(256) void k_lengths(GKState st, const int64_t* __re
 // correct, only less balanced).  Runs before k_ingest on the same HIP stream.
 // ===========================================================================
 #define GK_SORT_LONG_MAX 4096
+// k_ingest_wg (below): at most this many streams per call, each with at least
+// GK_WG_MIN_FLUSHES presorted flushes
+#ifndef GK_WG_MAX
+#define GK_WG_MAX 16
+#endif
+#ifndef GK_WG_MIN_FLUSHES
+#define GK_WG_MIN_FLUSHES 256
+#endif
+#define GK_WG_CAP 2048
+#define GK_WG_PMAX 1024
 #ifndef GK_PRESORT_REL
 #define GK_PRESORT_REL 3  // presort streams with >= 1/GK_PRESORT_REL of the longest one's flushes
 #endif
@@ -328,7 +338,8 @@ __global__ __launch_bounds__(1024) void k_long_prep(GKState st, const int64_t* _
                                                     int32_t* __restrict__ list, int64_t* __restrict__ list_n,
                                                     const int32_t* __restrict__ count,
                                                     int64_t* __restrict__ list_ws, int64_t* __restrict__ list_b0,
-                                                    int64_t ws_cap, int64_t* __restrict__ ws_need) {
+                                                    int64_t ws_cap, int64_t* __restrict__ ws_need,
+                                                    int32_t* __restrict__ wg_count) {
   __shared__ uint64_t key[GK_SORT_LONG_MAX];
   const int cnt = *count;
   const int t = threadIdx.x;
@@ -420,6 +431,18 @@ __global__ __launch_bounds__(1024) void k_long_prep(GKState st, const int64_t* _
     list_b0[i] = b;
     list_ws[i] = (nb > 0 && (b + nb) * st.P <= ws_cap) ? b * st.P : -1;
     b += nb;
+  }
+  // k_ingest_wg's streams: the presorted head of the list (longest first)
+  // with at least GK_WG_MIN_FLUSHES flushes, at most GK_WG_MAX of them
+  if (wg_count) {
+    __syncthreads();
+    if (t == 0) {
+      int k = 0;
+      while (k < cnt && k < GK_WG_MAX && list_ws[k] >= 0 &&
+             list_b0[k + 1 < cnt ? k + 1 : cnt] - list_b0[k] >= GK_WG_MIN_FLUSHES)
+        ++k;
+      *wg_count = st.cap[0] == GK_WG_CAP && st.P <= GK_WG_PMAX ? k : 0;
+    }
   }
 }
 
@@ -1402,7 +1425,12 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
                                                const int32_t* __restrict__ prio,
                                                const int32_t* __restrict__ prio_count,
                                                const double* __restrict__ psort,
-                                               const int64_t* __restrict__ prio_ws) {
+                                               const int64_t* __restrict__ prio_ws,
+                                               const int32_t* __restrict__ prio_skip) {
+  // the first *prio_skip streams of `prio` are k_ingest_wg's: skipped here,
+  // and as many blocks leave at once so that its workgroups find free CUs
+  const int skip = prio_skip ? *prio_skip : 0;
+  if (skip > 0 && (int)blockIdx.x >= (int)gridDim.x - skip && gridDim.x > (unsigned)skip) return;
   constexpr int LCAP = CAP > 0 ? CAP : 1;
   constexpr int LVPL = CAP > 0 ? VPL : 1;
   __shared__ FlushLDS<LCAP, LVPL> Ls;
@@ -1430,7 +1458,7 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
   // items [npri, npri+count) are the launch's streams in order, minus those
   // already taken from `prio` (the same length test k_lengths applied).
   if (count_ptr) count = *count_ptr;
-  const int64_t npri = prio ? (int64_t)*prio_count : 0;
+  const int64_t npri = prio ? max((int64_t)*prio_count - skip, (int64_t)0) : 0;
   const int64_t total = npri + count;
   auto grab = [&]() -> int64_t {
     unsigned long long v = 0;
@@ -1438,7 +1466,7 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
     return rfl64((int64_t)v);
   };
   auto sid = [&](int64_t w) -> int64_t {
-    return w < npri ? (int64_t)prio[w] : (list ? (int64_t)list[w - npri] : w - npri);
+    return w < npri ? (int64_t)prio[w + skip] : (list ? (int64_t)list[w - npri] : w - npri);
   };
   GKHdrV hv;
   int64_t w = grab();
@@ -1447,7 +1475,7 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
     const int64_t s = sid(w);
     const bool from_prio = w < npri;
     // presorted automatic-flush batches of this stream (k_presort), or none
-    const int64_t wso = (from_prio && prio_ws) ? rfl64(prio_ws[w]) : -1;
+    const int64_t wso = (from_prio && prio_ws) ? rfl64(prio_ws[w + skip]) : -1;
     const int64_t wn = grab();
     const int32_t scls = __builtin_amdgcn_readfirstlane(hv.cls);
     const int32_t sslot = __builtin_amdgcn_readfirstlane(hv.slot);
@@ -1610,6 +1638,397 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
   if (lane == 0)
     for (int i = 0; i < GK_PROF_NSEC; ++i) atomicAdd(&gk_prof_acc[i], gk_big_prof().acc[i]);
 #endif
+}
+
+// ===========================================================================
+// k_ingest_wg: the longest streams of a batch, one WORKGROUP per stream
+// (round 4).  A Zipf head (cfg5: one stream of 10^7
+// values at eps = 0.001, 9 990 dependent flushes of 1 001 values) is a
+// sequential chain of flushes; one wave walked it at ~11.4 us per presorted
+// flush, the whole batch's critical path.  Here GK_WG_WAVES waves share each
+// flush: one or two batch values per thread, a few table entries per thread,
+// the carry walk resolved wave by wave (DPP) and across waves through LDS,
+// one workgroup scan for the output offsets.  Same closed form and results
+// as flush_wave (bit-exact; tests/test_gpu_wg.py).  Streams: the first
+// *wg_count entries of the long list (k_long_prep: presorted streams with
+// at least 1/GK_PRESORT_REL of the longest one's flushes, at most
+// GK_WG_MAX); class-0 sets of the 2048 class (128 < P <= 1024) only.
+// Batches arrive presorted (k_presort); a batch that is not (the call's
+// final partial flush) is sorted here by (value, insertion index) first.
+// The fused query of these streams is answered after the join by
+// k_query_list (their _min/_max are final only then), so none here.
+// ===========================================================================
+#ifndef GK_WG_WAVES
+#define GK_WG_WAVES 8
+#endif
+#define GK_WG_T (64 * GK_WG_WAVES)
+#define GK_WG_VPT ((GK_WG_PMAX + GK_WG_T - 1) / GK_WG_T)
+
+struct WgLDS {
+  double tv[2][GK_WG_CAP];
+  int32_t tg[2][GK_WG_CAP];
+  int32_t td[2][GK_WG_CAP];
+  uint32_t gpk[GK_WG_CAP + 1];  // per gap: count, then (member base << 16) | out base
+  int32_t gk[GK_WG_CAP + 1];    // per entry: absorbed count | KEEP bit
+  int32_t gdel[GK_WG_CAP + 1];  // per entry: G, then G + d - 1
+  double sv[GK_WG_PMAX];        // sort area of an unsorted batch
+  uint32_t si[GK_WG_PMAX];
+  uint32_t wsum[GK_WG_WAVES];   // the scan's wave totals
+  int32_t xdone[GK_WG_WAVES], xc[GK_WG_WAVES];  // the carry walk's wave-boundary states
+  uint32_t total;
+};
+
+// values q = t + GK_WG_T * r of a batch of cnt in ascending (value, insertion
+// index) order: Python's stable sorted() of gk:71-72
+__device__ __forceinline__ void wg_sort(WgLDS& L, double (&xv)[GK_WG_VPT], int cnt, int t) {
+  int N = 64;
+  while (N < cnt) N <<= 1;
+#pragma unroll
+  for (int r = 0; r < GK_WG_VPT; ++r) {
+    const int q = t + GK_WG_T * r;
+    if (q < N) {
+      L.sv[q] = q < cnt ? xv[r] : __longlong_as_double(0x7ff0000000000000LL);
+      L.si[q] = q < cnt ? (uint32_t)q : 0xffffffffu;
+    }
+  }
+  __syncthreads();
+  for (int k = 2; k <= N; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int pp = t; pp < N / 2; pp += GK_WG_T) {
+        const int a = ((pp & ~(j - 1)) << 1) | (pp & (j - 1));
+        const int c = a + j;
+        const double va = L.sv[a], vc = L.sv[c];
+        const uint32_t ia = L.si[a], ic = L.si[c];
+        const bool a_gt = (va > vc) || (!(va < vc) && ia > ic);
+        if (a_gt == ((a & k) == 0)) {
+          L.sv[a] = vc;
+          L.sv[c] = va;
+          L.si[a] = ic;
+          L.si[c] = ia;
+        }
+      }
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < GK_WG_VPT; ++r) {
+    const int q = t + GK_WG_T * r;
+    xv[r] = q < cnt ? L.sv[q] : 0.0;
+  }
+  __syncthreads();
+}
+
+// One flush of a sorted batch (value q of the batch in xv[r], q = t +
+// GK_WG_T*r) into the table in buffer `cur`; the new table goes to cur^1.
+// Returns the new size, or -1 if it would not fit GK_WG_CAP - 1 (nothing is
+// written to the global table then; the caller promotes the stream).
+__device__ int flush_wg(WgLDS& L, const int cur, const int E, const double (&xv)[GK_WG_VPT], const int cnt,
+                        const int T, const int t) {
+  const int lane = t & 63, w = t >> 6;
+  const double* __restrict__ tv = L.tv[cur];
+  const int32_t* __restrict__ tg = L.tg[cur];
+  const int32_t* __restrict__ td = L.td[cur];
+  double* __restrict__ nv = L.tv[cur ^ 1];
+  int32_t* __restrict__ ng = L.tg[cur ^ 1];
+  int32_t* __restrict__ nd = L.td[cur ^ 1];
+  // ---- gap = #entries <= x (gk:93), branch-free over the +inf-padded table
+  int xg[GK_WG_VPT];
+#pragma unroll
+  for (int r = 0; r < GK_WG_VPT; ++r) xg[r] = 0;
+  for (int step = gk_pow2_above(E) >> 1; step > 0; step >>= 1) {
+    double tt[GK_WG_VPT];
+#pragma unroll
+    for (int r = 0; r < GK_WG_VPT; ++r) tt[r] = tv[xg[r] + step - 1];
+#pragma unroll
+    for (int r = 0; r < GK_WG_VPT; ++r) xg[r] += (tt[r] <= xv[r]) ? step : 0;
+  }
+#pragma unroll
+  for (int r = 0; r < GK_WG_VPT; ++r) xg[r] = min(xg[r], E);
+  for (int j = t; j <= E; j += GK_WG_T) L.gpk[j] = 0u;
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < GK_WG_VPT; ++r)
+    if (t + GK_WG_T * r < cnt) atomicAdd(&L.gpk[xg[r]], 1u);
+  __syncthreads();
+
+  // ---- carry walk (closed form of gk:93-106) -----------------------------
+  // thread t owns entries [t*K, t*K+K); its carry-in is known at once when
+  // its predecessor entry is kept even at carry 0 (G grows with the carry);
+  // otherwise it waits for its left neighbour: inside a wave over DPP,
+  // across waves through LDS (one barrier per round; rounds are the longest
+  // chain of removed entries crossing a wave boundary, usually none)
+  const int K = (E + GK_WG_T - 1) / GK_WG_T;
+  const int j0 = t * K;
+  const int jend = min(j0 + K, E);
+  const bool has = j0 < E;
+  const int cs = T > 1 ? T : 1;
+  const int tail_t = E == 0 ? 0 : (E - 1) / K;
+  bool known = (t == 0) || !has;
+  if (has && t > 0) {
+    const int jp = j0 - 1;
+    const int g = tg[jp], d = td[jp], m = (int)L.gpk[jp];
+    const int G0 = g + clampi(T - d - g, 0, m);
+    known = !(G0 + tg[j0] + td[j0] <= T);
+  }
+  bool done = !has;
+  int cin = 0, cout = 0;
+  for (;;) {
+    for (;;) {
+      if (known && !done) {
+        int c = cin;
+        for (int j = j0; j < jend; ++j) {
+          const int g = tg[j], d = td[j], m = (int)L.gpk[j];
+          const int Gp = g + c;
+          const int k = clampi(T - d - Gp, 0, m);
+          const int G = Gp + k;
+          const bool rem = (j + 1 < E) && (G + tg[j + 1] + td[j + 1] <= T);
+          L.gk[j] = k | (rem ? 0 : GK_KEEP_BIT);
+          L.gdel[j] = G;
+          c = rem ? G : 0;
+        }
+        cout = c;
+        done = true;
+      }
+      const int pc = wave_shr1(cout, 0);
+      const int pd = wave_shr1((int)done, 1);
+      const bool nk = !known && lane > 0 && pd;
+      if (nk) {
+        known = true;
+        cin = pc;
+      }
+      if (__builtin_amdgcn_ballot_w64(nk) == 0) break;
+    }
+    if (lane == 63) {
+      L.xdone[w] = done ? 1 : 0;
+      L.xc[w] = cout;
+    }
+    __syncthreads();
+    if (lane == 0 && w > 0 && !known && L.xdone[w - 1]) {
+      known = true;
+      cin = L.xc[w - 1];
+    }
+    if (__syncthreads_and(done ? 1 : 0)) break;
+  }
+
+  // ---- output offsets: one workgroup scan of (members << 16 | outputs) -----
+  uint32_t sm = 0, so = 0;
+  for (int j = j0; j < jend; ++j) {
+    const int m = (int)L.gpk[j];
+    const int kk = L.gk[j];
+    sm += (uint32_t)m;
+    so += (uint32_t)(m - (kk & ~GK_KEEP_BIT) + ((kk & GK_KEEP_BIT) ? 1 : 0));
+  }
+  if (t == tail_t) {
+    const int mE = (int)L.gpk[E];
+    sm += (uint32_t)mE;
+    so += (uint32_t)((mE + cs - 1) / cs);
+  }
+  const uint32_t v = (sm << 16) | so;
+  const uint32_t incl = wave_incl_scan_u32(v, lane);
+  if (lane == 63) L.wsum[w] = incl;
+  __syncthreads();
+  uint32_t pre = 0, total = 0;
+#pragma unroll
+  for (int k = 0; k < GK_WG_WAVES; ++k) {
+    const uint32_t s = L.wsum[k];
+    pre += k < w ? s : 0u;
+    total += s;
+  }
+  const int newE = (int)(total & 0xffffu);
+  if (newE > GK_WG_CAP - 1) return -1;  // (uniform: total comes from LDS) one slot stays free for the padding
+  const int totm = (int)(total >> 16);
+  {
+    uint32_t base = pre + incl - v;
+    for (int j = j0; j < jend; ++j) {
+      const int m = (int)L.gpk[j];
+      const int kk = L.gk[j];
+      const int k = kk & ~GK_KEEP_BIT;
+      const int G = L.gdel[j];
+      const int d = td[j];
+      L.gpk[j] = base;
+      L.gdel[j] = G + d - 1;
+      if (kk & GK_KEEP_BIT) {
+        const int pos = (int)(base & 0xffffu) + m - k;
+        nv[pos] = tv[j];
+        ng[pos] = G;
+        nd[pos] = d;
+      }
+      base += ((uint32_t)m << 16) | (uint32_t)(m - k + ((kk & GK_KEEP_BIT) ? 1 : 0));
+    }
+    if (t == tail_t) L.gpk[E] = base;
+  }
+  __syncthreads();
+
+  // ---- the values: sorted, so the rank inside a gap is the position minus
+  //      the gap's member base (gk:93-99 for a gap before an entry, gk:85-92
+  //      for the tail: chunks of max(T,1), each emitting its last value)
+#pragma unroll
+  for (int r = 0; r < GK_WG_VPT; ++r) {
+    const int q = t + GK_WG_T * r;
+    if (q < cnt) {
+      const int gap = xg[r];
+      const uint32_t pk = L.gpk[gap];
+      const int rk = q - (int)(pk >> 16);
+      if (gap < E) {
+        const int k = L.gk[gap] & ~GK_KEEP_BIT;
+        if (rk >= k) {
+          const int pos = (int)(pk & 0xffffu) + rk - k;
+          nv[pos] = xv[r];
+          ng[pos] = 1;
+          nd[pos] = L.gdel[gap];
+        }
+      } else {
+        const int m = totm - (int)(pk >> 16);
+        const int qq = rk / cs;
+        const int rr = rk - qq * cs;
+        if (rr == cs - 1 || rk == m - 1) {
+          const int pos = (int)(pk & 0xffffu) + qq;
+          nv[pos] = xv[r];
+          ng[pos] = rr + 1;
+          nd[pos] = 0;
+        }
+      }
+    }
+  }
+  // +inf padding for the next search, up to pow2_above(newE) - 2
+  const int hi = gk_pow2_above(newE) - 1;
+  for (int j = newE + t; j < hi; j += GK_WG_T) nv[j] = __longlong_as_double(0x7ff0000000000000LL);
+  __syncthreads();
+  return newE;
+}
+
+__global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double* __restrict__ x,
+                                                       const int64_t* __restrict__ offs,
+                                                       const int32_t* __restrict__ prio,
+                                                       const int32_t* __restrict__ wg_count, int lcls, int force,
+                                                       int32_t* __restrict__ ovf_count,
+                                                       int32_t* __restrict__ ovf_list,
+                                                       unsigned long long* __restrict__ work,
+                                                       const double* __restrict__ psort,
+                                                       const int64_t* __restrict__ prio_ws) {
+  __shared__ WgLDS L;
+  __shared__ int64_t item;
+  const int t = threadIdx.x;
+  const int P = st.P;
+  const int64_t K = *wg_count;
+  for (;;) {
+    if (t == 0) item = (int64_t)atomicAdd(work, 1ull);
+    __syncthreads();
+    const int64_t wi = item;
+    __syncthreads();  // (item is rewritten by the next grab)
+    if (wi >= K) break;
+    const int64_t s = prio[wi];
+    const int32_t scls = st.cls[s];
+    if (scls != lcls) continue;  // in another class: handled by that class's launch
+    const int32_t sslot = st.slot[s];
+    int p = st.pend[s];
+    int E = st.E[s];
+    int64_t n = st.n[s];
+    const int64_t xo = offs[s];
+    const int64_t Lx = offs[s + 1] - xo;
+    const int64_t wso = prio_ws ? prio_ws[wi] : -1;
+    if (Lx <= 0 && !((force == 1 && p > 0) || (force == 2 && n > 0))) continue;
+    GKRec* __restrict__ tab = gk_table_ptr_cs(st, s, scls, sslot);
+    double* __restrict__ pb = st.pbuf + s * (int64_t)st.pmax;
+    bool ok = E <= GK_WG_CAP - 1 && P <= GK_WG_PMAX && gk_count_ok(st, n + (Lx > 0 ? Lx : 0));
+    int cur = 0;
+    if (ok) {
+      for (int j = t; j < E; j += GK_WG_T) {
+        const GKRec rc = tab[j];
+        L.tv[0][j] = rc.v;
+        L.tg[0][j] = rc.g;
+        L.td[0][j] = rc.d;
+      }
+      const int hi = gk_pow2_above(E) - 1;
+      for (int j = E + t; j < hi; j += GK_WG_T) L.tv[0][j] = __longlong_as_double(0x7ff0000000000000LL);
+    }
+    __syncthreads();
+    int64_t used = 0;
+    int64_t need = P - (n % P);  // adds until n hits the next multiple of P (gk:60)
+    bool flushed = false;
+    // presorted batch b of this call at psort + wso + b*P (k_presort)
+    const double* __restrict__ sb = wso >= 0 ? psort + wso : nullptr;
+    double xv[GK_WG_VPT];
+    while (ok && used + need <= Lx) {
+      const int cnt = p + (int)need;
+      if (sb) {
+#pragma unroll
+        for (int r = 0; r < GK_WG_VPT; ++r) {
+          const int q = t + GK_WG_T * r;
+          xv[r] = q < cnt ? sb[q] : 0.0;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < GK_WG_VPT; ++r) {
+          const int q = t + GK_WG_T * r;
+          xv[r] = q < cnt ? (q < p ? pb[q] : x[xo + used + (q - p)]) : 0.0;
+        }
+        wg_sort(L, xv, cnt, t);
+      }
+      n += need;
+      const int nE = flush_wg(L, cur, E, xv, cnt, gk_threshold(st, n), t);
+      if (nE < 0) {
+        ok = false;
+        break;
+      }
+      E = nE;
+      cur ^= 1;
+      used += need;
+      p = 0;
+      need = P;
+      flushed = true;
+      if (sb) sb += P;  // batch b at wso + b*P (k_presort)
+    }
+    (void)flushed;
+    if (ok) {
+      const int64_t rem = Lx - used;  // < need: no automatic flush for these
+      if ((force == 1 && p + rem > 0) || force == 2) {
+        const int cnt = p + (int)rem;
+#pragma unroll
+        for (int r = 0; r < GK_WG_VPT; ++r) {
+          const int q = t + GK_WG_T * r;
+          xv[r] = q < cnt ? (q < p ? pb[q] : x[xo + used + (q - p)]) : 0.0;
+        }
+        wg_sort(L, xv, cnt, t);
+        n += rem;
+        const int nE = flush_wg(L, cur, E, xv, cnt, gk_threshold(st, n), t);
+        if (nE < 0) {
+          ok = false;
+        } else {
+          E = nE;
+          cur ^= 1;
+          p = 0;
+        }
+      } else {
+        for (int64_t i = t; i < rem; i += GK_WG_T) pb[p + i] = x[xo + used + i];
+        p += (int)rem;
+        n += rem;
+      }
+    }
+    if (!ok) {
+      // nothing written back: the stream keeps its pre-call state and is
+      // re-run in the next capacity class
+      if (t == 0) {
+        const int k = atomicAdd(ovf_count, 1);
+        ovf_list[k] = (int32_t)s;
+      }
+      __syncthreads();
+      continue;
+    }
+    for (int j = t; j < E; j += GK_WG_T) {
+      GKRec rc;
+      rc.v = L.tv[cur][j];
+      rc.g = L.tg[cur][j];
+      rc.d = L.td[cur][j];
+      tab[j] = rc;
+    }
+    if (t == 0) {
+      st.n[s] = n;
+      st.E[s] = E;
+      st.pend[s] = p;
+    }
+    __syncthreads();
+  }
 }
 
 // ===========================================================================
@@ -3779,7 +4198,7 @@ static hipError_t launch_ingest_t(const GKState& st, const double* x, const int6
                                   unsigned char* ws, size_t ws_bytes, int64_t ws_blocks,
                                   int32_t* ovf_count, int32_t* ovf_list, const GKQuery& q,
                                   unsigned long long* work, const int32_t* prio, const int32_t* prio_count,
-                                  const double* psort, const int64_t* prio_ws, hipStream_t stream) {
+                                  const double* psort, const int64_t* prio_ws, const int32_t* prio_skip, hipStream_t stream) {
   if (count <= 0 && !count_ptr) return hipSuccess;
   if (!work) return hipErrorInvalidValue;
   int64_t grid;
@@ -3796,7 +4215,7 @@ static hipError_t launch_ingest_t(const GKState& st, const double* x, const int6
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL((k_ingest<CAP, VPL>), dim3((unsigned)grid), dim3(64), 0, stream, st, x, offs, list,
                      count, count_ptr, lcls, force, cap, ws, ws_bytes, ovf_count, ovf_list, q.qs, q.nq, q.out,
-                     q.mode, work, prio, prio_count, psort, prio_ws);
+                     q.mode, work, prio, prio_count, psort, prio_ws, prio_skip);
   return hipGetLastError();
 }
 
@@ -3806,10 +4225,10 @@ static hipError_t launch_ingest_vpl(int vpl, const GKState& st, const double* x,
                                     int force, int cap, unsigned char* ws,
                                     size_t ws_bytes, int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list,
                                     const GKQuery& q, unsigned long long* work, const int32_t* prio,
-                                    const int32_t* prio_count, const double* psort, const int64_t* prio_ws,
+                                    const int32_t* prio_count, const double* psort, const int64_t* prio_ws, const int32_t* prio_skip,
                                     hipStream_t stream) {
 #define GK_L(V) launch_ingest_t<CAP, V>(st, x, offs, list, count, count_ptr, lcls, force, cap, ws, ws_bytes, ws_blocks, \
-                                        ovf_count, ovf_list, q, work, prio, prio_count, psort, prio_ws, stream)
+                                        ovf_count, ovf_list, q, work, prio, prio_count, psort, prio_ws, prio_skip, stream)
   switch (vpl) {
     case 1: return GK_L(1);
     case 2: return GK_L(2);
@@ -3882,7 +4301,8 @@ hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x
                             unsigned char* ws, size_t ws_bytes,
                             int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list, const GKQuery& q,
                             unsigned long long* work, const int32_t* prio, const int32_t* prio_count,
-                            const double* psort, const int64_t* prio_ws, int fused_stats, hipStream_t stream) {
+                            const double* psort, const int64_t* prio_ws, const int32_t* prio_skip, int fused_stats,
+                            hipStream_t stream) {
   switch (cap) {
     case SMALL_CAP:
       if (list || count_ptr || lcls != 0) return hipErrorInvalidValue;  // class 0 over every stream only
@@ -3893,12 +4313,23 @@ hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x
       return hipErrorInvalidValue;
     case 2048:
       return launch_ingest_vpl<2048>(vpl, st, x, offs, list, count, count_ptr, lcls, force, cap, nullptr, 0, 0,
-                                     ovf_count, ovf_list, q, work, prio, prio_count, psort, prio_ws, stream);
+                                     ovf_count, ovf_list, q, work, prio, prio_count, psort, prio_ws, prio_skip, stream);
     default:
       if (!ws || ws_blocks <= 0) return hipErrorInvalidValue;
       return launch_ingest_vpl<0>(vpl, st, x, offs, list, count, count_ptr, lcls, force, cap, ws, ws_bytes,
-                                  ws_blocks, ovf_count, ovf_list, q, work, prio, prio_count, psort, prio_ws, stream);
+                                  ws_blocks, ovf_count, ovf_list, q, work, prio, prio_count, psort, prio_ws, prio_skip, stream);
   }
+}
+
+hipError_t gk_launch_ingest_wg(const GKState& st, const double* x, const int64_t* offs, const int32_t* long_list,
+                               const int32_t* wg_count, int lcls, int force, int32_t* ovf_count, int32_t* ovf_list,
+                               unsigned long long* work, const GKPresort& ps, hipStream_t stream) {
+  if (st.S <= 0 || !ps.wg_count || !work) return hipSuccess;
+  // (at most GK_WG_MAX streams: the count is only known on the device; the
+  // spare workgroups find the hand-out exhausted and leave)
+  hipLaunchKernelGGL(k_ingest_wg, dim3(GK_WG_MAX), dim3(GK_WG_T), 0, stream, st, x, offs, long_list, wg_count, lcls,
+                     force, ovf_count, ovf_list, work, (const double*)ps.ws, (const int64_t*)ps.list_ws);
+  return hipGetLastError();
 }
 
 hipError_t gk_launch_stats(const GKState& st, const int64_t* offs, int32_t* long_list, int64_t* long_n,
@@ -3911,7 +4342,7 @@ hipError_t gk_launch_stats(const GKState& st, const int64_t* offs, int32_t* long
   // (gk_launch_stats_short) run on this stream
   hipLaunchKernelGGL(k_lengths, dim3((unsigned)grid), dim3(256), 0, stream, st, offs, long_list, long_count);
   hipLaunchKernelGGL(k_long_prep, dim3(1), dim3(1024), 0, stream, st, offs, long_list, long_n,
-                     (const int32_t*)long_count, ps.list_ws, ps.list_b0, ps.ws_cap, ps.ws_need);
+                     (const int32_t*)long_count, ps.list_ws, ps.list_b0, ps.ws_cap, ps.ws_need, ps.wg_count);
   return hipGetLastError();
 }
 

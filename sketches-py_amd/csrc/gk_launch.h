@@ -54,7 +54,8 @@ hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x
                             unsigned char* ws, size_t ws_bytes,
                             int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list, const GKQuery& q,
                             unsigned long long* work, const int32_t* prio, const int32_t* prio_count,
-                            const double* psort, const int64_t* prio_ws, int fused_stats, hipStream_t stream);
+                            const double* psort, const int64_t* prio_ws, const int32_t* prio_skip, int fused_stats,
+                            hipStream_t stream);
 // The unbounded class (tables beyond 32768 entries; every class when P > 1024):
 // one wave per stream over ws (ws_bytes >= gk_big_ws_bytes(cap, P) per block,
 // ws_blocks blocks); list / count / count_ptr / lcls / force / q as above;
@@ -84,7 +85,13 @@ struct GKPresort {
   double* ws = nullptr;
   int64_t ws_cap = 0;
   int64_t* ws_need = nullptr;  // device, 1 value
+  int32_t* wg_count = nullptr; // device, 1 value: k_ingest_wg's streams (the head of the long list); NULL: none
 };
+// one workgroup per stream for the first *wg_count streams of the long list
+// (class lcls = 0 of the 2048 class only); the prio k_ingest launch skips them
+hipError_t gk_launch_ingest_wg(const GKState& st, const double* x, const int64_t* offs, const int32_t* long_list,
+                               const int32_t* wg_count, int lcls, int force, int32_t* ovf_count, int32_t* ovf_list,
+                               unsigned long long* work, const GKPresort& ps, hipStream_t stream);
 // the long-stream list + pre-call n (k_lengths), then k_long_prep
 hipError_t gk_launch_stats(const GKState& st, const int64_t* offs, int32_t* long_list, int64_t* long_n,
                            int32_t* long_count, const GKPresort& ps, hipStream_t stream);
@@ -167,6 +174,7 @@ hipError_t gk_launch_promote(const GKState& st, const int32_t* list, int64_t cou
 #define GK_CTR_RCNT 16    // [16 + 4*round + class]
 #define GK_CTR_OVFC 40    // [40 + round]
 #define GK_CTR_BADPEND 48 // gk_import: streams with an unreachable pending count
+#define GK_CTR_WG 50      // k_ingest_wg's stream count this call (k_long_prep)
 #define GK_CTR_WORDS 16
 #define GK_CTR_CALL 14
 #define GK_CALL_WORK 256                          // bytes: the small-class launch's GK_WORK_BYTES, then

@@ -1,0 +1,101 @@
+"""k_ingest_wg (round 4): the longest presorted streams of
+a batch run one WORKGROUP per stream (the flush of gk:63-109 shared by 8
+waves), beside the one-wave-per-stream class-0 launch, which skips them.
+
+Parity bar: every stream's table, pending values, n/min/max/sum/avg and the
+fused quantiles bit-identical to the C oracle and to the same calls with the
+path switched off (GK_WG=0), over several calls (the presort workspace exists
+from the second call on, so the path engages then) with pending values carried
+between calls, ties, signed zeros, and one adversarial (descending) long
+stream whose table outgrows the 2048 class inside k_ingest_wg (promoted and
+re-run in the next class).  GK_WG_TRACE=1 shows on stderr how many streams
+the path took per call: it must be > 0."""
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from gk_oracle_c import OracleSet
+from parity_util import _ss, assert_same_quantiles, assert_same_state, small_of
+
+pytestmark = pytest.mark.gpu
+
+EPS = 0.001
+QS = [0.0, 0.01, 0.5, 0.9, 0.999, 1.0]
+
+
+def batches(seed):
+    """Three calls over 200 streams: 5 long ones (300-700 flushes of 1001
+    values per call, >= GK_WG_MIN_FLUSHES = 256), one descending long stream,
+    the rest short; lengths not multiples of P (pending values carry over)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for call in range(3):
+        lens = rng.integers(0, 4000, 200)
+        lens[:5] = rng.integers(300_000, 700_000, 5)
+        lens[7] = 400_000
+        seqs = [rng.lognormal(0.0, 1.5, int(L)) for L in lens]
+        seqs[1] = np.round(seqs[1], 1)  # ties
+        seqs[2][::97] = 0.0
+        seqs[2][::89] = -0.0  # signed zeros
+        if call > 0:  # descending from the second call (k_ingest_wg's first): outgrows 2048 inside it
+            seqs[7] = np.linspace(1e6 - call * 1e5, 1.0 - call * 1e5, int(lens[7]))
+        out.append(seqs)
+    return out
+
+
+def run(dev, monkeypatch, env, calls):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    ss = _ss(200, EPS, dev)
+    res = []
+    for seqs in calls:
+        offs = np.zeros(201, np.int64)
+        offs[1:] = np.cumsum([len(x) for x in seqs])
+        x = torch.from_numpy(np.concatenate(seqs)).to(dev)
+        q = ss.ingest(x, torch.from_numpy(offs).to(dev), quantiles=QS).cpu().numpy()
+        res.append((q, offs))
+    return ss, res
+
+
+def test_wg_streams_match_oracle_and_one_wave_path(gpu_device, monkeypatch, capfd):
+    calls = batches(5)
+    ss, res = run(gpu_device, monkeypatch, {"GK_WG": "1", "GK_WG_TRACE": "1"}, calls)
+    err = capfd.readouterr().err
+    took = [int(m) for m in re.findall(r"k_ingest_wg: (\d+) stream", err)]
+    assert took and max(took) > 0, "k_ingest_wg took no stream: %r" % err[-2000:]
+    ss_off, res_off = run(gpu_device, monkeypatch, {"GK_WG": "0"}, calls)
+    o = OracleSet(200, EPS)
+    for (q, offs), (q_off, _), seqs in zip(res, res_off, calls):
+        o.ingest(np.concatenate(seqs), offs)
+        assert np.array_equal(q.view(np.int64), q_off.view(np.int64)), "wg vs one-wave path quantiles"
+        assert_same_quantiles(q, o.quantiles(QS), "wg quantiles vs oracle", small_of(o, EPS))
+    assert_same_state(ss, o, "wg path")
+    assert_same_state(ss_off, o, "one-wave path")
+    assert ss.num_promoted >= 1  # the descending stream left the 2048 class
+
+
+def test_wg_plain_ingest_then_query(gpu_device, monkeypatch, capfd):
+    """Ingest without a fused query (pending values stay pending), then a
+    separate quantiles() call flushes them: wg path vs oracle."""
+    monkeypatch.setenv("GK_WG", "1")
+    monkeypatch.setenv("GK_WG_TRACE", "1")
+    rng = np.random.default_rng(9)
+    ss = _ss(40, EPS, gpu_device)
+    o = OracleSet(40, EPS)
+    for call in range(3):
+        lens = rng.integers(0, 3000, 40)
+        lens[0] = 520_123 + call
+        lens[3] = 333_333
+        seqs = [rng.random(int(L)) for L in lens]
+        offs = np.zeros(41, np.int64)
+        offs[1:] = np.cumsum(lens)
+        flat = np.concatenate(seqs)
+        ss.ingest(torch.from_numpy(flat).to(gpu_device), torch.from_numpy(offs).to(gpu_device))
+        o.ingest(flat, offs)
+        assert_same_state(ss, o, "call %d" % call)
+    took = [int(m) for m in re.findall(r"k_ingest_wg: (\d+) stream", capfd.readouterr().err)]
+    assert took and max(took) > 0
+    assert_same_quantiles(ss.quantiles(QS).cpu().numpy(), o.quantiles(QS), "final query", small_of(o, EPS))
+    assert_same_state(ss, o, "after query")
