@@ -21,7 +21,14 @@
  *    re-run by the device itself.  Part of an ingest (the sequential
  *    _sum/_avg chains of streams longer than 16384 values) runs on a stream
  *    the set owns; `stream` is made to wait for it, so every later call
- *    enqueued on `stream` sees the finished state.  The caller keeps input
+ *    enqueued on `stream` sees the finished state.  The chains of the few
+ *    longest streams (>= 2^20 values) are walked on host cores by a worker
+ *    thread of the set: the call only hands them over (it does not block)
+ *    and `stream` waits for the worker on the device (a kernel polling a
+ *    pinned flag, bounded at 20 s; a failed host walk is redone on the
+ *    device, same bits).  The set's next call, gk_sync and gk_destroy first
+ *    wait for that worker on the host.  While `stream` is being captured
+ *    into a graph, no chain is handed to the host.  The caller keeps input
  *    buffers alive and unchanged until the set's next call or gk_sync: a
  *    stream that needs a class whose arena has no free slot yet is deferred
  *    and re-run from them by the host runtime before the next call proceeds.
