@@ -24,6 +24,19 @@ for rep in 1 2; do
     python3 -c "import json,sys; d=json.loads(open('gpurun_out/${TAG}_ab.tmp').read().strip().splitlines()[-1]); print('%-32s %7.2f Gv/s  ms/step %.3f  launch_ms %.3f  frac %.3f' % (sys.argv[1], d['value']/1e9, d['ms_per_step'], d['roofline']['launch_ms'], d['roofline']['frac']))" "$lib" | tee -a gpurun_out/${TAG}_ab.txt
   done
 done
+# the two-streams-per-wave experiment (GK_HALF=1): parity first, then the bench
+GK_HALF=1 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_dist.py -m gpu -q --timeout 200 --timeout-method thread > gpurun_out/${TAG}_half_tests.log 2>&1
+rc=$?
+echo "GK_HALF=1 tests rc=$rc: $(tail -1 gpurun_out/${TAG}_half_tests.log)" | tee -a gpurun_out/${TAG}_ab.txt
+if [ $rc -gt 1 ]; then echo "abort (rc $rc)"; exit 1; fi
+if [ $rc -eq 0 ]; then
+  for rep in 1 2; do
+    for lib in libgkarray_hip.so libgkarray_hip_h5.so; do
+      GK_HALF=1 GK_LIB_PATH=sketches-py_amd/gkarray_amd/$lib timeout -k 10 200 python bench.py --no-cpu --steps 10 --warmup 3 > gpurun_out/${TAG}_ab.tmp 2>&1 || { echo "FAILED half: $lib"; tail -20 gpurun_out/${TAG}_ab.tmp; exit 1; }
+      python3 -c "import json,sys; d=json.loads(open('gpurun_out/${TAG}_ab.tmp').read().strip().splitlines()[-1]); print('HALF %-27s %7.2f Gv/s  ms/step %.3f  launch_ms %.3f  frac %.3f' % (sys.argv[1], d['value']/1e9, d['ms_per_step'], d['roofline']['launch_ms'], d['roofline']['frac']))" "$lib" | tee -a gpurun_out/${TAG}_ab.txt
+    done
+  done
+fi
 for wg in 1 0; do
   GK_WG=$wg timeout -k 10 300 python bench.py --workload cfg5 --no-cpu --steps 5 --warmup 2 > gpurun_out/${TAG}_cfg5_wg$wg.json 2> gpurun_out/${TAG}_cfg5_wg$wg.err || { echo "cfg5 FAILED wg=$wg"; tail -20 gpurun_out/${TAG}_cfg5_wg$wg.err; exit 1; }
   python3 -c "import json,sys; d=json.loads(open('gpurun_out/${TAG}_cfg5_wg$wg.json').read().strip().splitlines()[-1]); print('cfg5 GK_WG=%s  %7.3f Gv/s  ms/step %.2f' % (sys.argv[1], d['value']/1e9, d['ms_per_step']))" "$wg" | tee -a gpurun_out/${TAG}_ab.txt

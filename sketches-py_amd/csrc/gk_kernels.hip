@@ -2413,6 +2413,9 @@ __global__ __launch_bounds__(64) void k_ingest_big(GKState st, const double* __r
 #ifndef GK_TPRED
 #define GK_TPRED 1  // T and its divider made one flush ahead
 #endif
+#ifndef GK_ZSEL
+#define GK_ZSEL 1  // zero only the count words a flush set
+#endif
 #ifndef GK_SMALL_WAVES
 #define GK_SMALL_WAVES 6  // min waves per SIMD asked of the register allocator
 #endif
@@ -3121,7 +3124,18 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
     GK_MARK(L, 6);
   }
   small_pad(L.tv, newE, lane);
+#if GK_ZSEL
+  // zero exactly the count words this flush can have set: every gap's
+  // count and record live at its padded index, and the lanes' pairs
+  // (pj0, pj0+1) cover every padded index but 32/65/98, which never hold a
+  // gap (the tail pE included); the exact rank pass's member indices (mi)
+  // only reach those words' .y halves and index 32.  One ds_write2_b32 per
+  // lane instead of 1 088 bytes of zeros.
+  L.gi[pj0].x = 0;
+  L.gi[pj0 + 1].x = 0;
+#else
   small_zero_counts(L.gi, lane);
+#endif
   if constexpr (GK_DUPG(12)) {
     dup_st(&L.tv[pidx(min(newE + lane, SMALL_CAP - 1))], __longlong_as_double(0x7ff0000000000000LL));
     small_zero_counts(L.gi, lane);
@@ -3614,6 +3628,11 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
     for (int i = 0; i < GK_PROF_NSEC; ++i) atomicAdd(&gk_prof_acc[i], L.prof[i]);
 #endif
 }
+
+#ifndef GK_HALF_WAVES
+#define GK_HALF_WAVES 4  // min waves per SIMD for k_ingest_half (128 VGPRs)
+#endif
+#include "gk_half.inc"
 
 // ===========================================================================
 // k_merge: GKArray.merge (gk:111-154) and merge_compress(entries), stream by
@@ -4265,7 +4284,24 @@ static hipError_t launch_ingest_small(const GKState& st, const double* x, const 
   const int pace = nstat > 0 && grid >= 4 * (int64_t)nstat && grid >= 8 * GK_WORK_PARTS ? 1 : 0;
   static const int lag = getenv("GK_FS_LAG") ? atoi(getenv("GK_FS_LAG")) : GK_FS_LAG_DEFAULT;
   if (list) return hipErrorInvalidValue;  // class 0 over every stream only
-  if (nstat > 0)
+  // GK_HALF=1: two streams per wave (k_ingest_half, experiment)
+  static const bool half = getenv("GK_HALF") && atoi(getenv("GK_HALF")) != 0;
+  if (half) {
+    int hocc = 0;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&hocc, k_ingest_half<false>, 64, 0);
+    if (hocc <= 0) hocc = 1;
+    int64_t hgrid = (int64_t)num_cu() * hocc;
+    if (hgrid > (count + 1) / 2) hgrid = (count + 1) / 2;
+    if (hgrid < 1) hgrid = 1;
+    if (nstat > hgrid) nstat = (int)hgrid;
+    const int hpace = nstat > 0 && hgrid >= 4 * (int64_t)nstat && hgrid >= 8 * GK_WORK_PARTS ? 1 : 0;
+    if (nstat > 0)
+      hipLaunchKernelGGL((k_ingest_half<true>), dim3((unsigned)hgrid), dim3(64), 0, stream, st, x, offs, count,
+                         force, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode, work, nstat, hpace, lag);
+    else
+      hipLaunchKernelGGL((k_ingest_half<false>), dim3((unsigned)hgrid), dim3(64), 0, stream, st, x, offs, count,
+                         force, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode, work, nstat, hpace, lag);
+  } else if (nstat > 0)
     hipLaunchKernelGGL((k_ingest_small<VPL, true>), dim3((unsigned)grid), dim3(64), 0, stream, st, x, offs, count,
                        force, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode, work, nstat, pace, lag);
   else
