@@ -3257,6 +3257,7 @@ __device__ __attribute__((noinline)) double small_quantiles(SmallLDS<VPL>& L, in
 // streams -- so its reads of the values hit the L2 lines the ingest waves
 // (same XCD, same moment) fetched, instead of reading the batch from HBM a
 // second time.  pace == 0: no waiting (every wave may be a stats wave).
+template <int DEPTH = GK_FS_DEPTH>
 __device__ __forceinline__ void fused_stats_role(const GKState& st, const double* __restrict__ x,
                                                  const int64_t* __restrict__ offs,
                                                  unsigned long long* __restrict__ work, int part, int nparts,
@@ -3323,18 +3324,18 @@ __device__ __forceinline__ void fused_stats_role(const GKState& st, const double
     const bool uni = nu == rfl64(nhi) && nu >= 0 && nu + 8 * maxch + 8 < st.rtab_n;
     // loads past a lane's last chunk read the first aligned values of the
     // batch instead, so every refill is unconditional
-    double2 ring[GK_FS_DEPTH][4];
+    double2 ring[DEPTH][4];
 #pragma unroll
-    for (int d = 0; d < GK_FS_DEPTH; ++d) {
+    for (int d = 0; d < DEPTH; ++d) {
       const double2* src = (d < nch) ? p2 + d * 4 : dummy;
 #pragma unroll
       for (int j = 0; j < 4; ++j) ring[d][j] = src[j];
     }
     auto walk = [&](auto tab) {
       constexpr bool TAB = decltype(tab)::value;
-      for (int64_t c0 = 0; c0 < maxch; c0 += GK_FS_DEPTH) {
+      for (int64_t c0 = 0; c0 < maxch; c0 += DEPTH) {
 #pragma unroll
-        for (int d = 0; d < GK_FS_DEPTH; ++d) {
+        for (int d = 0; d < DEPTH; ++d) {
           const int64_t c = c0 + d;
           if (c < nch) {
             const double* __restrict__ rt = st.rtab + (nu + 8 * c + 1);  // uniform (TAB)
@@ -3349,7 +3350,7 @@ __device__ __forceinline__ void fused_stats_role(const GKState& st, const double
             }
             n += 8;                           // gk:52
           }
-          const int64_t nx = c + GK_FS_DEPTH;
+          const int64_t nx = c + DEPTH;
           const double2* src = (nx < nch) ? p2 + nx * 4 : dummy;
 #pragma unroll
           for (int j = 0; j < 4; ++j) ring[d][j] = src[j];
