@@ -199,6 +199,10 @@ int gk_load(gk_set* set, const char* path, void* stream);
  *                state of dst is replaced. */
 int gk_pack_bytes(gk_set* set, int64_t* bytes, void* stream);
 int gk_pack(gk_set* set, void* buf, int64_t bytes, void* stream);
+/* Each bufs[r] must hold the whole packed state its header describes (the
+ * header's byte count, as gk_pack_bytes returned it for the packing set):
+ * headers and offset tables are checked for consistency, but the buffers'
+ * own lengths are not known to this call. */
 int gk_fold_packed(gk_set* dst, const void* const* bufs, int nbufs, void* stream);
 
 /* Introspection for tests and benchmarks. */

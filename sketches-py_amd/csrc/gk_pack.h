@@ -176,8 +176,11 @@ int read_header(gk_set* dst, const void* buf, Header* h, void* stream, std::stri
           std::to_string(gk_num_streams(dst));
     return GK_E_ARG;
   }
-  // sizes and offsets: a truncated or corrupt buffer must not reach gk_import
-  // (whose copies would read past the buffer)
+  // sizes and offsets must be internally consistent before gk_import copies
+  // anything (a corrupt header or offset table is refused).  The buffer's
+  // own length is not known here (gk_fold_packed takes bare pointers): the
+  // caller guarantees each buffer holds the header's `bytes` (gk_capi.h) --
+  // a buffer truncated after an intact header and offset table is not caught
   if (h->E < 0 || h->P < 0 || h->E > ((int64_t)1 << 40) || h->P > ((int64_t)1 << 40) ||
       h->bytes != (int64_t)layout(h->S, h->E, h->P).total) {
     err = "packed state header is inconsistent (sizes / byte count)";
