@@ -323,7 +323,7 @@ __global__ __launch_bounds__(256) void k_lengths(GKState st, const int64_t* __re
 // k_ingest_wg (below): at most this many streams per call, each with at least
 // GK_WG_MIN_FLUSHES presorted flushes
 #ifndef GK_WG_MAX
-#define GK_WG_MAX 16
+#define GK_WG_MAX 64
 #endif
 #ifndef GK_WG_MIN_FLUSHES
 #define GK_WG_MIN_FLUSHES 256
@@ -332,6 +332,11 @@ __global__ __launch_bounds__(256) void k_lengths(GKState st, const int64_t* __re
 #define GK_WG_PMAX 1024
 #ifndef GK_PRESORT_REL
 #define GK_PRESORT_REL 3  // presort streams with >= 1/GK_PRESORT_REL of the longest one's flushes
+#endif
+// ... and with k_ingest_wg on (the longest streams walk ~3x faster there), the
+// one-wave path's critical length shrinks: presort down to 1/GK_PRESORT_REL_WG
+#ifndef GK_PRESORT_REL_WG
+#define GK_PRESORT_REL_WG 5
 #endif
 
 __global__ __launch_bounds__(1024) void k_long_prep(GKState st, const int64_t* __restrict__ offs,
@@ -406,7 +411,7 @@ __global__ __launch_bounds__(1024) void k_long_prep(GKState st, const int64_t* _
     atomicMax(&nbmax, (unsigned long long)nb);
   }
   __syncthreads();
-  const int64_t nb_min = (int64_t)(nbmax / GK_PRESORT_REL);
+  const int64_t nb_min = (int64_t)(nbmax / (wg_count ? GK_PRESORT_REL_WG : GK_PRESORT_REL));
   int64_t mine = 0;
   for (int i = i0; i < i1; ++i) {
     if (list_b0[i] < nb_min) list_b0[i] = 0;  // flushed unsorted
@@ -1949,9 +1954,16 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
     // presorted batch b of this call at psort + wso + b*P (k_presort)
     const double* __restrict__ sb = wso >= 0 ? psort + wso : nullptr;
     double xv[GK_WG_VPT];
+    // the next presorted batch is loaded one flush ahead (its HBM latency
+    // under the current flush); xn holds it
+    double xn[GK_WG_VPT];
+    bool have_next = false;
     while (ok && used + need <= Lx) {
       const int cnt = p + (int)need;
-      if (sb) {
+      if (sb && have_next) {
+#pragma unroll
+        for (int r = 0; r < GK_WG_VPT; ++r) xv[r] = xn[r];
+      } else if (sb) {
 #pragma unroll
         for (int r = 0; r < GK_WG_VPT; ++r) {
           const int q = t + GK_WG_T * r;
@@ -1966,6 +1978,15 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
         wg_sort(L, xv, cnt, t);
       }
       n += need;
+      // prefetch: the next automatic flush's presorted batch (P values at sb + P)
+      have_next = sb != nullptr && used + need + P <= Lx;
+      if (have_next) {
+#pragma unroll
+        for (int r = 0; r < GK_WG_VPT; ++r) {
+          const int q = t + GK_WG_T * r;
+          xn[r] = q < P ? sb[P + q] : 0.0;
+        }
+      }
       const int nE = flush_wg(L, cur, E, xv, cnt, gk_threshold(st, n), t);
       if (nE < 0) {
         ok = false;
