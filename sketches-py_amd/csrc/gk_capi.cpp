@@ -1073,8 +1073,9 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
     if (h->h_ws_need) *h->h_ws_need = 0;
     // the longest presorted streams: one workgroup each (k_ingest_wg, 2048
     // class, P <= 1024; GK_WG=0 turns it off); their count is a per-call word
-    bool wg = st.cap[0] == 2048 && h->P <= 1024;
-    if (const char* e = getenv("GK_WG")) wg = wg && atoi(e) != 0;
+    // (off by default until validated on a GPU: GK_WG=1 turns it on)
+    bool wg = false;
+    if (const char* e = getenv("GK_WG")) wg = st.cap[0] == 2048 && h->P <= 1024 && atoi(e) != 0;
     if (wg) h->ps.wg_count = h->d_ctr + GK_CTR_WG;
     h->wg_trace = getenv("GK_WG_TRACE") != nullptr;
     okm &= hipEventCreateWithFlags(&h->ev_wg, hipEventDisableTiming) == hipSuccess;
