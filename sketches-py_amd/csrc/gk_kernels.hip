@@ -2424,16 +2424,13 @@ __global__ __launch_bounds__(64) void k_ingest_big(GKState st, const double* __r
 //    prefix(g) + d - 1, one ballot + popcount per entry slot and quantile.
 // ===========================================================================
 #define SMALL_CAP GK_SMALL_CAP
-// Round-4 variants of the small class, OFF in the product build until a
-// GPU run has validated them (the round's GPU pool was unavailable for
-// hours; one of GD16 / DPP64 / TPRED failed the row-shard fold test in the
-// one run that happened -- bisect pending).  Variant builds enable them.
+// Round-4 variants of the small class, measured on MI355X and left OFF in
+// the product build (profiles/r04f_ab.txt, cfg3 k_ingest_small launch vs
+// 5.98-5.99 ms): GD16 6.06-6.09 ms (+1.4%: fewer LDS cycles, more VALU and
+// a longer chain), TPRED 6.06 ms (+1.2%), ZSEL 5.92-6.00 ms (within noise).
 // entry (g, d) of the LDS table packed in 32 bits (1) or as two int32 (0)
 #ifndef GK_GD16
 #define GK_GD16 0
-#endif
-#ifndef GK_DPP64
-#define GK_DPP64 0  // register sort: 64-bit DPP partner moves
 #endif
 #ifndef GK_TPRED
 #define GK_TPRED 0  // T and its divider made one flush ahead
@@ -2595,12 +2592,10 @@ __device__ __forceinline__ CsDiv make_csdiv(int T) {
   return c;
 }
 
-#if GK_GD16
 // (g, d) <-> the packed LDS word: g in bits 0-15, d in bits 16-31 (one v_perm_b32)
 __device__ __forceinline__ uint32_t gd_pack(int g, int d) { return __builtin_amdgcn_perm((uint32_t)d, (uint32_t)g, 0x05040100u); }
 __device__ __forceinline__ int gd_g(uint32_t w) { return (int)(w & 0xffffu); }
 __device__ __forceinline__ int gd_d(uint32_t w) { return (int)(w >> 16); }
-#endif
 
 template <int VPL, int DUPG = -1>
 __device__ __forceinline__ void small_put(SmallLDS<VPL>& L, int pos, double v, int g, int d) {
@@ -2659,25 +2654,9 @@ __device__ __forceinline__ int lane_xor_i32(int v, int lane) {
 
 template <int J>
 __device__ __forceinline__ double lane_xor_f64(double v, int lane) {
-  // pure DPP partners as one 64-bit DPP move: both halves land in a register
-  // pair (per 32-bit half the compiler copied one half into the pair: an
-  // extra v_mov per compare-exchange)
-  if constexpr (!GK_DPP64)
-    return __hiloint2double(lane_xor_i32<J>(__double2hiint(v), lane), lane_xor_i32<J>(__double2loint(v), lane));
-  else if constexpr (J == 1) return __builtin_amdgcn_mov_dpp(v, GK_DPP_QPERM(1, 0, 3, 2), 0xf, 0xf, true);
-  else if constexpr (J == 2) return __builtin_amdgcn_mov_dpp(v, GK_DPP_QPERM(2, 3, 0, 1), 0xf, 0xf, true);
-  else if constexpr (J == 3) return __builtin_amdgcn_mov_dpp(v, GK_DPP_QPERM(3, 2, 1, 0), 0xf, 0xf, true);
-  else if constexpr (J == 7) return __builtin_amdgcn_mov_dpp(v, GK_DPP_ROW_HALF_MIRROR, 0xf, 0xf, true);
-  else if constexpr (J == 15) return __builtin_amdgcn_mov_dpp(v, GK_DPP_ROW_MIRROR, 0xf, 0xf, true);
-  else if constexpr (J == 8) return __builtin_amdgcn_mov_dpp(v, GK_DPP_ROW_ROR8, 0xf, 0xf, true);
-  else if constexpr (J == 4)
-    return __builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp(v, GK_DPP_ROW_HALF_MIRROR, 0xf, 0xf, true),
-                                    GK_DPP_QPERM(3, 2, 1, 0), 0xf, 0xf, true);
-  else if constexpr (J == 31) {
-    const double m = __builtin_amdgcn_mov_dpp(v, GK_DPP_ROW_MIRROR, 0xf, 0xf, true);
-    return __hiloint2double(gk_xor16(__double2hiint(m), lane), gk_xor16(__double2loint(m), lane));
-  } else
-    return __hiloint2double(lane_xor_i32<J>(__double2hiint(v), lane), lane_xor_i32<J>(__double2loint(v), lane));
+  // (round 4: one 64-bit DPP move per pair instead of two 32-bit ones saved a
+  // v_mov per compare-exchange but gave wrong sorts on the GPU -- reverted)
+  return __hiloint2double(lane_xor_i32<J>(__double2hiint(v), lane), lane_xor_i32<J>(__double2loint(v), lane));
 }
 
 // a[r] against the value at lane ^ X (same r); the lower lane (bit LB of the
@@ -3658,9 +3637,7 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
 #ifndef GK_HALF_WAVES
 #define GK_HALF_WAVES 4  // min waves per SIMD for k_ingest_half (128 VGPRs)
 #endif
-#if GK_GD16
 #include "gk_half.inc"
-#endif
 
 // ===========================================================================
 // k_merge: GKArray.merge (gk:111-154) and merge_compress(entries), stream by
@@ -4313,13 +4290,8 @@ static hipError_t launch_ingest_small(const GKState& st, const double* x, const 
   static const int lag = getenv("GK_FS_LAG") ? atoi(getenv("GK_FS_LAG")) : GK_FS_LAG_DEFAULT;
   if (list) return hipErrorInvalidValue;  // class 0 over every stream only
   // GK_HALF=1: two streams per wave (k_ingest_half, experiment)
-#if GK_GD16
   static const bool half = getenv("GK_HALF") && atoi(getenv("GK_HALF")) != 0;
-#else
-  constexpr bool half = false;  // (k_ingest_half needs the packed (g, d) layout)
-#endif
   if (half) {
-#if GK_GD16
     int hocc = 0;
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&hocc, k_ingest_half<false>, 64, 0);
     if (hocc <= 0) hocc = 1;
@@ -4334,7 +4306,6 @@ static hipError_t launch_ingest_small(const GKState& st, const double* x, const 
     else
       hipLaunchKernelGGL((k_ingest_half<false>), dim3((unsigned)hgrid), dim3(64), 0, stream, st, x, offs, count,
                          force, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode, work, nstat, hpace, lag);
-#endif
   } else if (nstat > 0)
     hipLaunchKernelGGL((k_ingest_small<VPL, true>), dim3((unsigned)grid), dim3(64), 0, stream, st, x, offs, count,
                        force, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode, work, nstat, pace, lag);
