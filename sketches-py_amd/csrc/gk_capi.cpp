@@ -829,10 +829,15 @@ int run_ingest(gk_set* h, const double* x, const int64_t* offs, int force, hipSt
   if (t0) HIP_TRY(hipEventRecord(t0, stream));
   // the longest presorted streams of an ingest: one workgroup each, on aux2
   // right behind their presort, beside the class-0 launch (which skips them)
-  const bool wg = prio && x != nullptr && h->ps.wg_count && h->aux2 && h->ps.list_ws && h->ps.ws && h->ps.ws_cap > 0;
+  const bool wg = prio && x != nullptr && h->ps.wg_count && h->aux2 && h->ps.list_ws &&
+                  (!h->ps.wg_presort || (h->ps.ws && h->ps.ws_cap > 0));
   if (wg) {
     unsigned long long* wwork = work_counter(h, false);
     if (!wwork) return fail(GK_E_HIP, "no hand-out counter left for k_ingest_wg");
+    // (behind k_long_prep, which counts its streams, and the call's counter
+    // reset: the fork point; the presort, when there is one, is already
+    // ordered after it on aux2)
+    HIP_TRY(hipStreamWaitEvent(h->aux2, h->ev_fork, 0));
     HIP_TRY(gk_launch_ingest_wg(h->st, x, offs, h->d_long_list, h->ps.wg_count, 0, force, ovf_count(h, 0),
                                 ovf_list(h, 0), wwork, h->ps, h->aux2));
     HIP_TRY(hipEventRecord(h->ev_wg, h->aux2));
@@ -1077,6 +1082,7 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
     bool wg = false;
     if (const char* e = getenv("GK_WG")) wg = st.cap[0] == 2048 && h->P <= 1024 && atoi(e) != 0;
     if (wg) h->ps.wg_count = h->d_ctr + GK_CTR_WG;
+    if (const char* e = getenv("GK_WG_PRESORT")) h->ps.wg_presort = atoi(e) != 0;
     h->wg_trace = getenv("GK_WG_TRACE") != nullptr;
     okm &= hipEventCreateWithFlags(&h->ev_wg, hipEventDisableTiming) == hipSuccess;
   }

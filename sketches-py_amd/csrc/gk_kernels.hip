@@ -108,6 +108,7 @@ __device__ __forceinline__ int clamp0(int x, int m) {
 // DPP controls (GFX9 family, gfx950 included)
 #define DPP_ROW_SHR(n) (0x110 + (n))
 #define DPP_WAVE_SHR1 0x138
+#define DPP_WAVE_SHL1 0x130
 #define DPP_ROW_BCAST15 0x142
 #define DPP_ROW_BCAST31 0x143
 
@@ -344,7 +345,7 @@ __global__ __launch_bounds__(1024) void k_long_prep(GKState st, const int64_t* _
                                                     const int32_t* __restrict__ count,
                                                     int64_t* __restrict__ list_ws, int64_t* __restrict__ list_b0,
                                                     int64_t ws_cap, int64_t* __restrict__ ws_need,
-                                                    int32_t* __restrict__ wg_count) {
+                                                    int32_t* __restrict__ wg_count, int wg_presort) {
   __shared__ uint64_t key[GK_SORT_LONG_MAX];
   const int cnt = *count;
   const int t = threadIdx.x;
@@ -411,6 +412,25 @@ __global__ __launch_bounds__(1024) void k_long_prep(GKState st, const int64_t* _
     atomicMax(&nbmax, (unsigned long long)nb);
   }
   __syncthreads();
+  if (wg_count && !wg_presort) {
+    // k_ingest_wg takes the head of the list (longest first: every stream
+    // with at least GK_WG_MIN_FLUSHES flushes, at most GK_WG_MAX) and ranks
+    // its unsorted batches itself; the one-wave path's streams are then
+    // short enough to flush unsorted: nothing is presorted
+    if (t == 0) {
+      int k = 0;
+      while (k < cnt && k < GK_WG_MAX && list_b0[k] >= GK_WG_MIN_FLUSHES) ++k;
+      *wg_count = st.cap[0] == GK_WG_CAP && st.P <= GK_WG_PMAX ? k : 0;
+      *ws_need = 0;
+    }
+    __syncthreads();
+    for (int i = i0; i < i1; ++i) {
+      list_ws[i] = -1;
+      list_b0[i] = 0;
+    }
+    if (t == 0) list_b0[cnt] = 0;
+    return;
+  }
   const int64_t nb_min = (int64_t)(nbmax / (wg_count ? GK_PRESORT_REL_WG : GK_PRESORT_REL));
   int64_t mine = 0;
   for (int i = i0; i < i1; ++i) {
@@ -675,7 +695,119 @@ __device__ __forceinline__ void gk_stat_step(double v, int64_t& n, double& sm, d
 }
 
 
-// one wave walks stream list[w] (the broadcast layout)
+// ---------------------------------------------------------------------------
+// Speculative walk of one stream's _sum/_avg chains (round 4).  The chains
+// are sequential (gk:53-54: every value's update reads the previous result,
+// three float64 roundings per _avg step), so one lane walks them at the
+// latency of its dependent ops, ~16 ns/value.  A superstep of 64 x W values
+// runs them on all 64 lanes at once instead:
+//  1. lane j takes values j*W .. j*W+W-1 and starts from an ESTIMATE of the
+//     chain at its first value (lane 0: the true value; lane j > 0: the
+//     running mean/sum continued with a tree sum of the lanes before it);
+//  2. each lane walks its W steps from its estimate (spec values X[0..W]);
+//  3. the spec values are shifted onto the true chain: lane j's offset D_j
+//     from a lane scan of X_{j-1}[W] - X_j[0] (lane 0: D = 0), b_t = X_t + D_j;
+//  4. every step is CHECKED in parallel, bit for bit: f(b_t) == b_{t+1}
+//     (lane j's b_W is lane j+1's b_0).  If every check passes, by induction
+//     from the true b_0 every b_t is the sequential chain's value.  At the
+//     first failing step the true value there is f(b_t): the checks restart
+//     from it (only the steps after it), so each round makes progress and
+//     the result is bit-exact whatever the data; usually one round suffices
+//     (an offset keeps the _avg roundings unless the update crosses a
+//     rounding boundary; the _sum's only at a binade change or a tie).
+// tools/mb/spec_chain.c is the host prototype (rounds per superstep:
+// lognormal 1.01-1.10, Pareto 1.08, signed e^+-50 3.3, all bit-exact).
+// ---------------------------------------------------------------------------
+#ifndef GK_SPEC_W
+#define GK_SPEC_W 16
+#endif
+#ifndef GK_SPEC
+#define GK_SPEC 1
+#endif
+#ifndef GK_SPEC_ROUNDS
+#define GK_SPEC_ROUNDS 16
+#endif
+
+// inclusive wave64 prefix sum of doubles on DPP (lanes without a source add
+// +0.0); the addition order is the scan's, not a sequential one
+__device__ __forceinline__ double wave_incl_scan_f64(double v) {
+#define GK_SCAN_STEP(C, M) v = v + __longlong_as_double(dpp64<C, M>(__double_as_longlong(v), 0))
+  GK_SCAN_STEP(DPP_ROW_SHR(1), 0xf);
+  GK_SCAN_STEP(DPP_ROW_SHR(2), 0xf);
+  GK_SCAN_STEP(DPP_ROW_SHR(4), 0xf);
+  GK_SCAN_STEP(DPP_ROW_SHR(8), 0xf);
+  GK_SCAN_STEP(DPP_ROW_BCAST15, 0xa);
+  GK_SCAN_STEP(DPP_ROW_BCAST31, 0xc);
+#undef GK_SCAN_STEP
+  return v;
+}
+// the value of lane-1 / lane+1 (lane 0 / lane 63: fill)
+__device__ __forceinline__ double wave_shr1_f64(double v, double fill) {
+  return __longlong_as_double(dpp64<DPP_WAVE_SHR1, 0xf>(__double_as_longlong(v), __double_as_longlong(fill)));
+}
+__device__ __forceinline__ double wave_shl1_f64(double v, double fill) {
+  return __longlong_as_double(dpp64<DPP_WAVE_SHL1, 0xf>(__double_as_longlong(v), __double_as_longlong(fill)));
+}
+
+__device__ __forceinline__ double rdlane_f64(double v, int l) {
+  const int64_t b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(uint32_t)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double((int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+
+// KIND 0: _avg (b + (v - b) * r), 1: _sum (b + v).  X: this lane's spec
+// values, K: the true value before the superstep.  Returns the true value
+// after it (wave-uniform), or ok = false after GK_SPEC_ROUNDS rounds.
+template <int KIND, int W>
+__device__ __forceinline__ double spec_verify(const double (&X)[W + 1], const double (&v)[W], const double (&r)[W],
+                                              double K, int lane, bool& ok) {
+  int jo = 0, to = 0;  // first step not yet verified (lane, step); K = the true value there
+  for (int round = 0;; ++round) {
+    if (round == GK_SPEC_ROUNDS) {  // pathological data (infinities, NaNs): the caller walks it one at a time
+      ok = false;
+      return K;
+    }
+    double xt = X[0];
+#pragma unroll
+    for (int t = 1; t < W; ++t)
+      if (t == to) xt = X[t];
+    const double xprev = wave_shr1_f64(X[W], 0.0);
+    const double D = wave_incl_scan_f64(lane < jo ? 0.0 : (lane == jo ? K - xt : xprev - X[0]));
+    const double b0 = (lane == jo && to == 0) ? K : X[0] + D;
+    const double bnx = wave_shl1_f64(b0, 0.0);  // lane j+1's b_0
+    int ft = W;
+    double fv = 0.0;
+    double b = b0;
+#pragma unroll
+    for (int t = 0; t < W; ++t) {
+      double bn = (t + 1 < W || lane == 63) ? X[t + 1] + D : bnx;
+      if (lane == jo && t + 1 == to) bn = K;
+      const double f = KIND == 0 ? b + (v[t] - b) * r[t] : b + v[t];
+      const bool act = lane > jo || (lane == jo && t >= to);
+      if (act && ft == W && __double_as_longlong(f) != __double_as_longlong(bn)) {
+        ft = t;
+        fv = f;
+      }
+      b = bn;
+    }
+    const uint64_t bad = __builtin_amdgcn_ballot_w64(ft < W);
+    if (!bad) return rdlane_f64(X[W] + D, 63);
+    const int jf = __builtin_amdgcn_readfirstlane(__builtin_ffsll((long long)bad) - 1);
+    const int tf = __builtin_amdgcn_readlane(ft, jf);
+    K = rdlane_f64(fv, jf);
+    jo = jf;
+    to = tf + 1;
+    if (to == W) {
+      ++jo;
+      to = 0;
+      if (jo == 64) return K;
+    }
+  }
+}
+
+// one wave walks stream list[w] (the broadcast layout): supersteps of 64 x
+// GK_SPEC_W values by the speculative walk above, the rest one value at a
+// time over LDS broadcasts
 __device__ __forceinline__ void stats_long_bcast(const GKState& st, const double* __restrict__ x,
                                                  const int64_t* __restrict__ offs, const int32_t* __restrict__ list,
                                                  const int64_t* __restrict__ list_n, int w, int lane, double2* buf) {
@@ -686,10 +818,72 @@ __device__ __forceinline__ void stats_long_bcast(const GKState& st, const double
   double sm = st.sum[s], av = st.avg[s];
   double lmn = __longlong_as_double(0x7ff0000000000000LL), lmx = -lmn;
   int64_t imn = INT64_MAX, imx = INT64_MAX;
+  int64_t kb = 0;  // first value of the one-at-a-time walk
+#if GK_SPEC
+  {
+    constexpr int W = GK_SPEC_W;
+    constexpr int SS = 64 * W;
+    double vn[W];
+    if (L >= SS) {
+#pragma unroll
+      for (int t = 0; t < W; ++t) vn[t] = x[xo + lane * W + t];
+    }
+    for (; kb + SS <= L; kb += SS) {
+      double v[W], r[W];
+#pragma unroll
+      for (int t = 0; t < W; ++t) v[t] = vn[t];
+      if (kb + 2 * SS <= L) {  // the next superstep's values, one superstep ahead
+#pragma unroll
+        for (int t = 0; t < W; ++t) vn[t] = x[xo + kb + SS + lane * W + t];
+      }
+      const int64_t i0 = kb + lane * W;  // this lane's first value (stream-relative)
+#pragma unroll
+      for (int t = 0; t < W; ++t) {
+        r[t] = 1.0 / (double)(n + i0 + t + 1 - kb);  // gk:54's 1.0/n
+        if (v[t] < lmn) { lmn = v[t]; imn = i0 + t; }  // gk:56-57 (first occurrence)
+        if (v[t] > lmx) { lmx = v[t]; imx = i0 + t; }  // gk:58-59
+      }
+      // estimates of both chains at this lane's first value
+      double p = 0.0;
+      {
+        double tr[W];
+#pragma unroll
+        for (int t = 0; t < W; ++t) tr[t] = v[t];
+#pragma unroll
+        for (int h = W / 2; h > 0; h >>= 1)
+#pragma unroll
+          for (int t = 0; t < h; ++t) tr[t] = tr[t] + tr[t + h];
+        p = tr[0];
+      }
+      // exclusive (an estimate: any value is correct, a close one saves rounds)
+      const double q = wave_incl_scan_f64(p) - p;
+      const int64_t nl = n + lane * W;
+      double ea = lane == 0 ? av : (av * (double)n + q) / (double)nl;
+      double es = lane == 0 ? sm : sm + q;
+      double XA[W + 1], XS[W + 1];
+      XA[0] = ea;
+      XS[0] = es;
+#pragma unroll
+      for (int t = 0; t < W; ++t) {
+        es = es + v[t];                // gk:53
+        ea = ea + (v[t] - ea) * r[t];  // gk:54
+        XA[t + 1] = ea;
+        XS[t + 1] = es;
+      }
+      bool ok = true;
+      const double av1 = spec_verify<0, W>(XA, v, r, av, lane, ok);
+      const double sm1 = ok ? spec_verify<1, W>(XS, v, r, sm, lane, ok) : sm;
+      if (!ok) break;  // this superstep and the rest one at a time (min/max re-seen: same indices, no change)
+      av = av1;
+      sm = sm1;
+      n += SS;  // gk:52
+    }
+  }
+#endif
   double q[SL_BCAST_DEPTH];
 #pragma unroll
-  for (int d = 0; d < SL_BCAST_DEPTH; ++d) q[d] = (64 * d + lane < L) ? x[xo + 64 * d + lane] : 0.0;
-  for (int64_t k0 = 0; k0 < L; k0 += 64 * SL_BCAST_DEPTH) {
+  for (int d = 0; d < SL_BCAST_DEPTH; ++d) q[d] = (kb + 64 * d + lane < L) ? x[xo + kb + 64 * d + lane] : 0.0;
+  for (int64_t k0 = kb; k0 < L; k0 += 64 * SL_BCAST_DEPTH) {
 #pragma unroll
     for (int d = 0; d < SL_BCAST_DEPTH; ++d) {
       const int64_t c0 = k0 + 64 * d;  // first index of this chunk
@@ -874,12 +1068,13 @@ __global__ __launch_bounds__(64) void k_stats_long(GKState st, const double* __r
                                                    const int32_t* __restrict__ list,
                                                    const int64_t* __restrict__ list_n,
                                                    const int32_t* __restrict__ count,
-                                                   const int32_t* __restrict__ hc_count) {
+                                                   const int32_t* __restrict__ hc_count, int prio) {
   __shared__ double2 buf[64];
   __shared__ double rtile[64];
   const int lane = threadIdx.x;
   const int cnt = *count;
   if (cnt <= GK_SL_BCAST) {
+    if (prio) __builtin_amdgcn_s_setprio(3);
     // the first *hc_count streams are walked on host cores (k_hc_prep)
     const int w0 = hc_count ? *hc_count : 0;
     for (int w = w0 + blockIdx.x; w < cnt; w += gridDim.x) stats_long_bcast(st, x, offs, list, list_n, w, lane, buf);
@@ -1723,12 +1918,19 @@ __device__ __forceinline__ void wg_sort(WgLDS& L, double (&xv)[GK_WG_VPT], int c
   __syncthreads();
 }
 
-// One flush of a sorted batch (value q of the batch in xv[r], q = t +
-// GK_WG_T*r) into the table in buffer `cur`; the new table goes to cur^1.
+// One flush of a batch (value q of the batch in xv[r], q = t + GK_WG_T*r)
+// into the table in buffer `cur`; the new table goes to cur^1.  A presorted
+// batch (sorted: ascending (value, insertion index)) places value q at rank
+// q - (its gap's first position); an unsorted one ranks each value among its
+// gap's members (stored by gap in the sort area; gaps hold ~P/E values, ~1 for
+// iid data), or, when some gap holds GK_WG_RANK_MAX or more, is sorted first.
 // Returns the new size, or -1 if it would not fit GK_WG_CAP - 1 (nothing is
 // written to the global table then; the caller promotes the stream).
-__device__ int flush_wg(WgLDS& L, const int cur, const int E, const double (&xv)[GK_WG_VPT], const int cnt,
-                        const int T, const int t) {
+#ifndef GK_WG_RANK_MAX
+#define GK_WG_RANK_MAX 32
+#endif
+__device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG_VPT], const int cnt,
+                        const int T, const int t, bool sorted) {
   const int lane = t & 63, w = t >> 6;
   const double* __restrict__ tv = L.tv[cur];
   const int32_t* __restrict__ tg = L.tg[cur];
@@ -1738,23 +1940,38 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, const double (&xv)
   int32_t* __restrict__ nd = L.td[cur ^ 1];
   // ---- gap = #entries <= x (gk:93), branch-free over the +inf-padded table
   int xg[GK_WG_VPT];
+  uint32_t slot[GK_WG_VPT];  // an unsorted value's member slot in its gap
+  for (;;) {
 #pragma unroll
-  for (int r = 0; r < GK_WG_VPT; ++r) xg[r] = 0;
-  for (int step = gk_pow2_above(E) >> 1; step > 0; step >>= 1) {
-    double tt[GK_WG_VPT];
+    for (int r = 0; r < GK_WG_VPT; ++r) xg[r] = 0;
+    for (int step = gk_pow2_above(E) >> 1; step > 0; step >>= 1) {
+      double tt[GK_WG_VPT];
 #pragma unroll
-    for (int r = 0; r < GK_WG_VPT; ++r) tt[r] = tv[xg[r] + step - 1];
+      for (int r = 0; r < GK_WG_VPT; ++r) tt[r] = tv[xg[r] + step - 1];
 #pragma unroll
-    for (int r = 0; r < GK_WG_VPT; ++r) xg[r] += (tt[r] <= xv[r]) ? step : 0;
+      for (int r = 0; r < GK_WG_VPT; ++r) xg[r] += (tt[r] <= xv[r]) ? step : 0;
+    }
+#pragma unroll
+    for (int r = 0; r < GK_WG_VPT; ++r) xg[r] = min(xg[r], E);
+    for (int j = t; j <= E; j += GK_WG_T) L.gpk[j] = 0u;
+    __syncthreads();
+    bool big = false;
+#pragma unroll
+    for (int r = 0; r < GK_WG_VPT; ++r) {
+      slot[r] = 0;
+      if (t + GK_WG_T * r < cnt) {
+        slot[r] = atomicAdd(&L.gpk[xg[r]], 1u);
+        big |= slot[r] >= GK_WG_RANK_MAX;
+      }
+    }
+    if (sorted) {
+      __syncthreads();
+      break;
+    }
+    if (!__syncthreads_or(big ? 1 : 0)) break;
+    wg_sort(L, xv, cnt, t);  // a crowded gap: sort, then search again
+    sorted = true;
   }
-#pragma unroll
-  for (int r = 0; r < GK_WG_VPT; ++r) xg[r] = min(xg[r], E);
-  for (int j = t; j <= E; j += GK_WG_T) L.gpk[j] = 0u;
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < GK_WG_VPT; ++r)
-    if (t + GK_WG_T * r < cnt) atomicAdd(&L.gpk[xg[r]], 1u);
-  __syncthreads();
 
   // ---- carry walk (closed form of gk:93-106) -----------------------------
   // thread t owns entries [t*K, t*K+K); its carry-in is known at once when
@@ -1863,17 +2080,41 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, const double (&xv)
     if (t == tail_t) L.gpk[E] = base;
   }
   __syncthreads();
+  if (!sorted) {  // members by gap, in slot order
+#pragma unroll
+    for (int r = 0; r < GK_WG_VPT; ++r) {
+      const int q = t + GK_WG_T * r;
+      if (q < cnt) {
+        const int pos = (int)(L.gpk[xg[r]] >> 16) + (int)slot[r];
+        L.sv[pos] = xv[r];
+        L.si[pos] = (uint32_t)q;
+      }
+    }
+    __syncthreads();
+  }
 
-  // ---- the values: sorted, so the rank inside a gap is the position minus
-  //      the gap's member base (gk:93-99 for a gap before an entry, gk:85-92
-  //      for the tail: chunks of max(T,1), each emitting its last value)
+  // ---- the values: the rank inside a gap is the position minus the gap's
+  //      member base when sorted, else the count of its members before it in
+  //      (value, insertion index) order (gk:71-72); gk:93-99 for a gap before
+  //      an entry, gk:85-92 for the tail: chunks of max(T,1), each emitting
+  //      its last value
 #pragma unroll
   for (int r = 0; r < GK_WG_VPT; ++r) {
     const int q = t + GK_WG_T * r;
     if (q < cnt) {
       const int gap = xg[r];
       const uint32_t pk = L.gpk[gap];
-      const int rk = q - (int)(pk >> 16);
+      int rk = q - (int)(pk >> 16);
+      if (!sorted) {
+        const int mb = (int)(pk >> 16);
+        const int me = gap < E ? (int)(L.gpk[gap + 1] >> 16) : totm;
+        const double xq = xv[r];
+        rk = 0;
+        for (int i = mb; i < me; ++i) {
+          const double u = L.sv[i];
+          rk += (u < xq || (!(xq < u) && L.si[i] < (uint32_t)q)) ? 1 : 0;
+        }
+      }
       if (gap < E) {
         const int k = L.gk[gap] & ~GK_KEEP_BIT;
         if (rk >= k) {
@@ -1954,13 +2195,13 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
     // presorted batch b of this call at psort + wso + b*P (k_presort)
     const double* __restrict__ sb = wso >= 0 ? psort + wso : nullptr;
     double xv[GK_WG_VPT];
-    // the next presorted batch is loaded one flush ahead (its HBM latency
-    // under the current flush); xn holds it
+    // the next batch is loaded one flush ahead (its HBM latency under the
+    // current flush); xn holds it
     double xn[GK_WG_VPT];
     bool have_next = false;
     while (ok && used + need <= Lx) {
       const int cnt = p + (int)need;
-      if (sb && have_next) {
+      if (have_next) {
 #pragma unroll
         for (int r = 0; r < GK_WG_VPT; ++r) xv[r] = xn[r];
       } else if (sb) {
@@ -1975,19 +2216,19 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
           const int q = t + GK_WG_T * r;
           xv[r] = q < cnt ? (q < p ? pb[q] : x[xo + used + (q - p)]) : 0.0;
         }
-        wg_sort(L, xv, cnt, t);
       }
       n += need;
-      // prefetch: the next automatic flush's presorted batch (P values at sb + P)
-      have_next = sb != nullptr && used + need + P <= Lx;
+      // prefetch: the next automatic flush's batch (P values: presorted at
+      // sb + P, or the call's next P values)
+      have_next = used + need + P <= Lx;
       if (have_next) {
 #pragma unroll
         for (int r = 0; r < GK_WG_VPT; ++r) {
           const int q = t + GK_WG_T * r;
-          xn[r] = q < P ? sb[P + q] : 0.0;
+          xn[r] = q < P ? (sb ? sb[P + q] : x[xo + used + need + q]) : 0.0;
         }
       }
-      const int nE = flush_wg(L, cur, E, xv, cnt, gk_threshold(st, n), t);
+      const int nE = flush_wg(L, cur, E, xv, cnt, gk_threshold(st, n), t, sb != nullptr);
       if (nE < 0) {
         ok = false;
         break;
@@ -2010,9 +2251,8 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
           const int q = t + GK_WG_T * r;
           xv[r] = q < cnt ? (q < p ? pb[q] : x[xo + used + (q - p)]) : 0.0;
         }
-        wg_sort(L, xv, cnt, t);
         n += rem;
-        const int nE = flush_wg(L, cur, E, xv, cnt, gk_threshold(st, n), t);
+        const int nE = flush_wg(L, cur, E, xv, cnt, gk_threshold(st, n), t, false);
         if (nE < 0) {
           ok = false;
         } else {
@@ -4383,7 +4623,8 @@ hipError_t gk_launch_stats(const GKState& st, const int64_t* offs, int32_t* long
   // (gk_launch_stats_short) run on this stream
   hipLaunchKernelGGL(k_lengths, dim3((unsigned)grid), dim3(256), 0, stream, st, offs, long_list, long_count);
   hipLaunchKernelGGL(k_long_prep, dim3(1), dim3(1024), 0, stream, st, offs, long_list, long_n,
-                     (const int32_t*)long_count, ps.list_ws, ps.list_b0, ps.ws_cap, ps.ws_need, ps.wg_count);
+                     (const int32_t*)long_count, ps.list_ws, ps.list_b0, ps.ws_cap, ps.ws_need, ps.wg_count,
+                     ps.wg_presort);
   return hipGetLastError();
 }
 
@@ -4410,8 +4651,12 @@ hipError_t gk_launch_stats_long(const GKState& st, const double* x, const int64_
   if (st.S <= 0) return hipSuccess;
   // the long-stream count is only known on the device: a fixed grid of waves
   // reads it (an empty list costs one short launch)
+  // (GK_SL_PRIO=0: the one-wave-per-stream walk without raised wave
+  // priority; with it the critical chains' waves win the SIMD's issue
+  // arbitration over the co-resident ingest waves)
+  static const int sl_prio = getenv("GK_SL_PRIO") ? atoi(getenv("GK_SL_PRIO")) : 1;
   hipLaunchKernelGGL(k_stats_long, dim3((unsigned)(num_cu() * 4)), dim3(64), 0, stream, st, x, offs, long_list,
-                     long_n, long_count, hc_count);
+                     long_n, long_count, hc_count, sl_prio);
   return hipGetLastError();
 }
 

@@ -4,8 +4,9 @@ waves), beside the one-wave-per-stream class-0 launch, which skips them.
 
 Parity bar: every stream's table, pending values, n/min/max/sum/avg and the
 fused quantiles bit-identical to the C oracle and to the same calls with the
-path switched off (GK_WG=0), over several calls (the presort workspace exists
-from the second call on, so the path engages then) with pending values carried
+path switched off (GK_WG=0), over several calls (with GK_WG_PRESORT=1 the
+presort workspace exists from the second call on, so the path engages then;
+by default the batches are not presorted and the path engages at once) with pending values carried
 between calls, ties, signed zeros, and one adversarial (descending) long
 stream whose table outgrows the 2048 class inside k_ingest_wg (promoted and
 re-run in the next class).  GK_WG_TRACE=1 shows on stderr how many streams
@@ -59,13 +60,17 @@ def run(dev, monkeypatch, env, calls):
     return ss, res
 
 
-def test_wg_streams_match_oracle_and_one_wave_path(gpu_device, monkeypatch, capfd):
+@pytest.mark.parametrize("presort", ["0", "1"])
+def test_wg_streams_match_oracle_and_one_wave_path(gpu_device, monkeypatch, capfd, presort):
+    """presort 0 (default): k_ingest_wg ranks unsorted batches among their
+    gaps' members (and sorts a batch with a crowded gap: the descending
+    stream's batches all fall below the table); 1: presorted batches."""
     calls = batches(5)
-    ss, res = run(gpu_device, monkeypatch, {"GK_WG": "1", "GK_WG_TRACE": "1"}, calls)
+    ss, res = run(gpu_device, monkeypatch, {"GK_WG": "1", "GK_WG_TRACE": "1", "GK_WG_PRESORT": presort}, calls)
     err = capfd.readouterr().err
     took = [int(m) for m in re.findall(r"k_ingest_wg: (\d+) stream", err)]
     assert took and max(took) > 0, "k_ingest_wg took no stream: %r" % err[-2000:]
-    ss_off, res_off = run(gpu_device, monkeypatch, {"GK_WG": "0"}, calls)
+    ss_off, res_off = run(gpu_device, monkeypatch, {"GK_WG": "0", "GK_WG_PRESORT": "0"}, calls)
     o = OracleSet(200, EPS)
     for (q, offs), (q_off, _), seqs in zip(res, res_off, calls):
         o.ingest(np.concatenate(seqs), offs)
