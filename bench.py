@@ -467,7 +467,8 @@ def main():
                    "streams_per_gpu": S_loc, "values_per_stream": L if a.workload != "cfg5" else N / max(S_loc, 1),
                    "eps": a.eps,
                    "parallelism": parallelism},
-        "roofline": {"bound": "hbm", "kernel": "k_ingest_small" if a.workload != "cfg5" else "k_ingest",
+        "roofline": {"bound": "hbm", "kernel": "k_ingest_small" if a.workload != "cfg5" else
+                     "k_ingest<2048> beside k_ingest_wg (the span of both)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
                      "traffic_ratio": ratio, "traffic_source": traffic_src,

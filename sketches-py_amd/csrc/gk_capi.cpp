@@ -740,7 +740,10 @@ int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s) {
     HIP_TRY(hipEventRecord(h->ev_presort, h->aux2));
   }
   if (!stats_fused(h)) HIP_TRY(gk_launch_stats_short(h->st, x, offs, s));
-  if (presort) HIP_TRY(hipStreamWaitEvent(s, h->ev_presort, 0));
+  // (with k_ingest_wg every presorted stream is one of its streams: the
+  // one-wave launch runs beside the presort; k_ingest_wg is ordered after it
+  // on aux2)
+  if (presort && !h->ps.wg_count) HIP_TRY(hipStreamWaitEvent(s, h->ev_presort, 0));
   if (h->ps.ws_need) HIP_TRY(hipMemcpyAsync(h->h_ws_need, h->ps.ws_need, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   hipEvent_t t1 = h->timing ? timing_event(h->tev_stats, h->n_stats) : nullptr;
   if (t1) HIP_TRY(hipEventRecord(t1, s));
@@ -829,8 +832,9 @@ int run_ingest(gk_set* h, const double* x, const int64_t* offs, int force, hipSt
   if (t0) HIP_TRY(hipEventRecord(t0, stream));
   // the longest presorted streams of an ingest: one workgroup each, on aux2
   // right behind their presort, beside the class-0 launch (which skips them)
-  const bool wg = prio && x != nullptr && h->ps.wg_count && h->aux2 && h->ps.list_ws &&
-                  (!h->ps.wg_presort || (h->ps.ws && h->ps.ws_cap > 0));
+  // (a stream whose batches are not presorted -- no workspace yet, or it did
+  // not fit -- is ranked unsorted there)
+  const bool wg = prio && x != nullptr && h->ps.wg_count && h->aux2 && h->ps.list_ws;
   if (wg) {
     unsigned long long* wwork = work_counter(h, false);
     if (!wwork) return fail(GK_E_HIP, "no hand-out counter left for k_ingest_wg");
@@ -843,10 +847,11 @@ int run_ingest(gk_set* h, const double* x, const int64_t* offs, int force, hipSt
     HIP_TRY(hipEventRecord(h->ev_wg, h->aux2));
   }
   HIP_TRY(launch_class(h, 0, x, offs, nullptr, nullptr, 0, force, q, stream, prio && x != nullptr, wg));
-  hipEvent_t t1 = timed ? timing_event(h->tev_flush, h->n_flush) : nullptr;
-  if (t1) HIP_TRY(hipEventRecord(t1, stream));
   // (its overflow entries feed the promotion rounds below)
   if (wg) HIP_TRY(hipStreamWaitEvent(stream, h->ev_wg, 0));
+  // (with k_ingest_wg beside it, the timed span is both: the call's batch ingest)
+  hipEvent_t t1 = timed ? timing_event(h->tev_flush, h->n_flush) : nullptr;
+  if (t1) HIP_TRY(hipEventRecord(t1, stream));
   if (!h->no_members)
     for (int c = 1; c < R; ++c)
       HIP_TRY(launch_class(h, c, x, offs, h->d_list[c], h->d_ctr + GK_CTR_LCNT + c, 0, force, q, stream));
@@ -948,10 +953,16 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
   h->device = device;
   h->vpl = h->P <= 1024 ? vpl_for(h->P) : 0;  // (registers of the capacity-class kernels)
   if (const char* fs = getenv("GK_FUSED_STATS")) h->fused_stats = std::max(0, std::min(64, atoi(fs)));
-  // host-walked chains: streams of >= 2^20 values (GK_HOST_CHAIN_MIN; 0 or
-  // GK_HOST_CHAINS=0: off) on up to 16 host threads (GK_HOST_CHAIN_THREADS;
-  // the process's CPU share: its affinity set, OMP_NUM_THREADS if lower)
-  h->hc_min = (int64_t)1 << 20;
+  // host-walked chains: off by default since round 4 (the device's
+  // speculative walk of k_stats_long runs a 10^7-value chain in a few ms,
+  // faster than a host core plus the PCIe copy of its values).  GK_HOST_CHAINS=1
+  // turns them on for streams of >= 2^20 values (GK_HOST_CHAIN_MIN sets the
+  // length and turns them on too; GK_HOST_CHAINS=0 wins) on up to 16 host
+  // threads (GK_HOST_CHAIN_THREADS; the process's CPU share: its affinity
+  // set, OMP_NUM_THREADS if lower)
+  h->hc_min = 0;
+  if (const char* e = getenv("GK_HOST_CHAINS"))
+    if (atoi(e) != 0) h->hc_min = (int64_t)1 << 20;
   if (const char* e = getenv("GK_HOST_CHAIN_MIN")) h->hc_min = std::max<int64_t>(0, atoll(e));
   if (const char* e = getenv("GK_HOST_CHAINS"))
     if (atoi(e) == 0) h->hc_min = 0;
@@ -1076,12 +1087,14 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
     okm &= hipMalloc(&h->ps.ws_need, sizeof(int64_t)) == hipSuccess;
     okm &= hipHostMalloc(&h->h_ws_need, sizeof(int64_t)) == hipSuccess;
     if (h->h_ws_need) *h->h_ws_need = 0;
-    // the longest presorted streams: one workgroup each (k_ingest_wg, 2048
-    // class, P <= 1024; GK_WG=0 turns it off); their count is a per-call word
-    // (off by default until validated on a GPU: GK_WG=1 turns it on)
-    bool wg = false;
-    if (const char* e = getenv("GK_WG")) wg = st.cap[0] == 2048 && h->P <= 1024 && atoi(e) != 0;
+    // the longest streams: one workgroup each (k_ingest_wg, 2048 class,
+    // P <= 1024; GK_WG=0 turns it off); their count is a per-call word.
+    // Their batches are presorted (GK_WG_PRESORT=0: not; k_ingest_wg then
+    // ranks each value among its gap's members)
+    bool wg = st.cap[0] == 2048 && h->P <= 1024;
+    if (const char* e = getenv("GK_WG")) wg = wg && atoi(e) != 0;
     if (wg) h->ps.wg_count = h->d_ctr + GK_CTR_WG;
+    h->ps.wg_presort = 1;
     if (const char* e = getenv("GK_WG_PRESORT")) h->ps.wg_presort = atoi(e) != 0;
     h->wg_trace = getenv("GK_WG_TRACE") != nullptr;
     okm &= hipEventCreateWithFlags(&h->ev_wg, hipEventDisableTiming) == hipSuccess;

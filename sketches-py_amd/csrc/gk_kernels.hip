@@ -412,29 +412,27 @@ __global__ __launch_bounds__(1024) void k_long_prep(GKState st, const int64_t* _
     atomicMax(&nbmax, (unsigned long long)nb);
   }
   __syncthreads();
-  if (wg_count && !wg_presort) {
-    // k_ingest_wg takes the head of the list (longest first: every stream
-    // with at least GK_WG_MIN_FLUSHES flushes, at most GK_WG_MAX) and ranks
-    // its unsorted batches itself; the one-wave path's streams are then
-    // short enough to flush unsorted: nothing is presorted
+  // k_ingest_wg takes the head of the list (longest first): every stream with
+  // at least GK_WG_MIN_FLUSHES flushes, at most GK_WG_MAX of them.  Only its
+  // streams are presorted then (GK_WG_PRESORT=0: none; k_ingest_wg ranks
+  // unsorted batches itself), so that the one-wave launch, whose streams are
+  // short enough to flush unsorted, need not wait for the presort
+  __shared__ int wk;
+  if (wg_count) {
     if (t == 0) {
       int k = 0;
       while (k < cnt && k < GK_WG_MAX && list_b0[k] >= GK_WG_MIN_FLUSHES) ++k;
-      *wg_count = st.cap[0] == GK_WG_CAP && st.P <= GK_WG_PMAX ? k : 0;
-      *ws_need = 0;
+      if (!(st.cap[0] == GK_WG_CAP && st.P <= GK_WG_PMAX)) k = 0;
+      *wg_count = k;
+      wk = wg_presort ? k : 0;
     }
     __syncthreads();
-    for (int i = i0; i < i1; ++i) {
-      list_ws[i] = -1;
-      list_b0[i] = 0;
-    }
-    if (t == 0) list_b0[cnt] = 0;
-    return;
   }
   const int64_t nb_min = (int64_t)(nbmax / (wg_count ? GK_PRESORT_REL_WG : GK_PRESORT_REL));
   int64_t mine = 0;
   for (int i = i0; i < i1; ++i) {
-    if (list_b0[i] < nb_min) list_b0[i] = 0;  // flushed unsorted
+    // flushed unsorted (with k_ingest_wg: all but its streams)
+    if (list_b0[i] < nb_min || (wg_count && i >= wk)) list_b0[i] = 0;
     mine += list_b0[i];
   }
   part[t] = mine;
@@ -456,18 +454,6 @@ __global__ __launch_bounds__(1024) void k_long_prep(GKState st, const int64_t* _
     list_b0[i] = b;
     list_ws[i] = (nb > 0 && (b + nb) * st.P <= ws_cap) ? b * st.P : -1;
     b += nb;
-  }
-  // k_ingest_wg's streams: the presorted head of the list (longest first)
-  // with at least GK_WG_MIN_FLUSHES flushes, at most GK_WG_MAX of them
-  if (wg_count) {
-    __syncthreads();
-    if (t == 0) {
-      int k = 0;
-      while (k < cnt && k < GK_WG_MAX && list_ws[k] >= 0 &&
-             list_b0[k + 1 < cnt ? k + 1 : cnt] - list_b0[k] >= GK_WG_MIN_FLUSHES)
-        ++k;
-      *wg_count = st.cap[0] == GK_WG_CAP && st.P <= GK_WG_PMAX ? k : 0;
-    }
   }
 }
 
@@ -1863,6 +1849,7 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
 #endif
 #define GK_WG_T (64 * GK_WG_WAVES)
 #define GK_WG_VPT ((GK_WG_PMAX + GK_WG_T - 1) / GK_WG_T)
+#define GK_WG_KMAX ((GK_WG_CAP + GK_WG_T - 1) / GK_WG_T)  // table entries per thread
 
 struct WgLDS {
   double tv[2][GK_WG_CAP];
@@ -1871,8 +1858,9 @@ struct WgLDS {
   uint32_t gpk[GK_WG_CAP + 1];  // per gap: count, then (member base << 16) | out base
   int32_t gk[GK_WG_CAP + 1];    // per entry: absorbed count | KEEP bit
   int32_t gdel[GK_WG_CAP + 1];  // per entry: G, then G + d - 1
-  double sv[GK_WG_PMAX];        // sort area of an unsorted batch
+  double sv[GK_WG_PMAX];        // sort area of a batch with a crowded gap
   uint32_t si[GK_WG_PMAX];
+  double2 mem[GK_WG_PMAX];      // an unsorted batch's values by gap: (value, insertion index bits)
   uint32_t wsum[GK_WG_WAVES];   // the scan's wave totals
   int32_t xdone[GK_WG_WAVES], xc[GK_WG_WAVES];  // the carry walk's wave-boundary states
   uint32_t total;
@@ -1929,6 +1917,9 @@ __device__ __forceinline__ void wg_sort(WgLDS& L, double (&xv)[GK_WG_VPT], int c
 #ifndef GK_WG_RANK_MAX
 #define GK_WG_RANK_MAX 32
 #endif
+#ifndef GK_WG_RK_UNROLL
+#define GK_WG_RK_UNROLL 4
+#endif
 __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG_VPT], const int cnt,
                         const int T, const int t, bool sorted) {
   const int lane = t & 63, w = t >> 6;
@@ -1969,56 +1960,83 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
       break;
     }
     if (!__syncthreads_or(big ? 1 : 0)) break;
+    GK_BMARK(2);
     wg_sort(L, xv, cnt, t);  // a crowded gap: sort, then search again
     sorted = true;
+    GK_BMARK(10);
   }
+  GK_BMARK(2);
 
   // ---- carry walk (closed form of gk:93-106) -----------------------------
-  // thread t owns entries [t*K, t*K+K); its carry-in is known at once when
-  // its predecessor entry is kept even at carry 0 (G grows with the carry);
-  // otherwise it waits for its left neighbour: inside a wave over DPP,
-  // across waves through LDS (one barrier per round; rounds are the longest
-  // chain of removed entries crossing a wave boundary, usually none)
+  // thread t owns entries [t*K, t*K+K) (K <= GK_WG_KMAX); their g, d and
+  // member counts are read into registers once, so that a carry chain that
+  // crosses many threads costs a few VALU per thread it crosses, not an LDS
+  // round trip.  A thread's carry-in is known at once when its predecessor
+  // entry is kept even at carry 0 (G grows with the carry); otherwise it
+  // waits for its left neighbour: inside a wave over DPP, across waves through
+  // LDS (one barrier per round; rounds are the longest chain of removed
+  // entries crossing a wave boundary, usually none)
+  constexpr int KM = GK_WG_KMAX;
   const int K = (E + GK_WG_T - 1) / GK_WG_T;
   const int j0 = t * K;
   const int jend = min(j0 + K, E);
+  const int nk = max(jend - j0, 0);
   const bool has = j0 < E;
   const int cs = T > 1 ? T : 1;
   const int tail_t = E == 0 ? 0 : (E - 1) / K;
+  int eg[KM], ed[KM], em[KM];
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    const bool in = k < nk;
+    eg[k] = in ? tg[j0 + k] : 0;
+    ed[k] = in ? td[j0 + k] : 0;
+    em[k] = in ? (int)L.gpk[j0 + k] : 0;
+  }
+  // the entry after this thread's block (the last entry's removal test)
+  const bool nx = has && jend < E;
+  const int gnx = nx ? tg[jend] : 0, dnx = nx ? td[jend] : 0;
   bool known = (t == 0) || !has;
   if (has && t > 0) {
     const int jp = j0 - 1;
     const int g = tg[jp], d = td[jp], m = (int)L.gpk[jp];
     const int G0 = g + clampi(T - d - g, 0, m);
-    known = !(G0 + tg[j0] + td[j0] <= T);
+    known = !(G0 + eg[0] + ed[0] <= T);
   }
   bool done = !has;
   int cin = 0, cout = 0;
+  int ek[KM], eG[KM];  // per entry: absorbed count | KEEP bit, G
+#pragma unroll
+  for (int k = 0; k < KM; ++k) ek[k] = eG[k] = 0;
   for (;;) {
     for (;;) {
       if (known && !done) {
         int c = cin;
-        for (int j = j0; j < jend; ++j) {
-          const int g = tg[j], d = td[j], m = (int)L.gpk[j];
-          const int Gp = g + c;
-          const int k = clampi(T - d - Gp, 0, m);
-          const int G = Gp + k;
-          const bool rem = (j + 1 < E) && (G + tg[j + 1] + td[j + 1] <= T);
-          L.gk[j] = k | (rem ? 0 : GK_KEEP_BIT);
-          L.gdel[j] = G;
-          c = rem ? G : 0;
+#pragma unroll
+        for (int k = 0; k < KM; ++k) {
+          if (k < nk) {
+            const int Gp = eg[k] + c;
+            const int kk = clampi(T - ed[k] - Gp, 0, em[k]);
+            const int G = Gp + kk;
+            const bool last = k + 1 >= nk;
+            const int gn = last ? gnx : eg[k + 1 < KM ? k + 1 : k];
+            const int dn = last ? dnx : ed[k + 1 < KM ? k + 1 : k];
+            const bool rem = (!last || nx) && (G + gn + dn <= T);
+            ek[k] = kk | (rem ? 0 : GK_KEEP_BIT);
+            eG[k] = G;
+            c = rem ? G : 0;
+          }
         }
         cout = c;
         done = true;
       }
       const int pc = wave_shr1(cout, 0);
       const int pd = wave_shr1((int)done, 1);
-      const bool nk = !known && lane > 0 && pd;
-      if (nk) {
+      const bool nkn = !known && lane > 0 && pd;
+      if (nkn) {
         known = true;
         cin = pc;
       }
-      if (__builtin_amdgcn_ballot_w64(nk) == 0) break;
+      if (__builtin_amdgcn_ballot_w64(nkn) == 0) break;
     }
     if (lane == 63) {
       L.xdone[w] = done ? 1 : 0;
@@ -2031,14 +2049,17 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
     }
     if (__syncthreads_and(done ? 1 : 0)) break;
   }
+  GK_BMARK(3);
 
   // ---- output offsets: one workgroup scan of (members << 16 | outputs) -----
   uint32_t sm = 0, so = 0;
-  for (int j = j0; j < jend; ++j) {
-    const int m = (int)L.gpk[j];
-    const int kk = L.gk[j];
-    sm += (uint32_t)m;
-    so += (uint32_t)(m - (kk & ~GK_KEEP_BIT) + ((kk & GK_KEEP_BIT) ? 1 : 0));
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    if (k < nk) {
+      const int m = em[k], kk = ek[k];
+      sm += (uint32_t)m;
+      so += (uint32_t)(m - (kk & ~GK_KEEP_BIT) + ((kk & GK_KEEP_BIT) ? 1 : 0));
+    }
   }
   if (t == tail_t) {
     const int mE = (int)L.gpk[E];
@@ -2061,60 +2082,93 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
   const int totm = (int)(total >> 16);
   {
     uint32_t base = pre + incl - v;
-    for (int j = j0; j < jend; ++j) {
-      const int m = (int)L.gpk[j];
-      const int kk = L.gk[j];
-      const int k = kk & ~GK_KEEP_BIT;
-      const int G = L.gdel[j];
-      const int d = td[j];
-      L.gpk[j] = base;
-      L.gdel[j] = G + d - 1;
-      if (kk & GK_KEEP_BIT) {
-        const int pos = (int)(base & 0xffffu) + m - k;
-        nv[pos] = tv[j];
-        ng[pos] = G;
-        nd[pos] = d;
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      if (k < nk) {
+        const int j = j0 + k;
+        const int m = em[k], kk = ek[k];
+        const int ka = kk & ~GK_KEEP_BIT;
+        const int G = eG[k];
+        const int d = ed[k];
+        L.gpk[j] = base;
+        L.gk[j] = kk;
+        L.gdel[j] = G + d - 1;
+        if (kk & GK_KEEP_BIT) {
+          const int pos = (int)(base & 0xffffu) + m - ka;
+          nv[pos] = tv[j];
+          ng[pos] = G;
+          nd[pos] = d;
+        }
+        base += ((uint32_t)m << 16) | (uint32_t)(m - ka + ((kk & GK_KEEP_BIT) ? 1 : 0));
       }
-      base += ((uint32_t)m << 16) | (uint32_t)(m - k + ((kk & GK_KEEP_BIT) ? 1 : 0));
     }
     if (t == tail_t) L.gpk[E] = base;
   }
   __syncthreads();
+  GK_BMARK(4);
   if (!sorted) {  // members by gap, in slot order
 #pragma unroll
     for (int r = 0; r < GK_WG_VPT; ++r) {
       const int q = t + GK_WG_T * r;
       if (q < cnt) {
         const int pos = (int)(L.gpk[xg[r]] >> 16) + (int)slot[r];
-        L.sv[pos] = xv[r];
-        L.si[pos] = (uint32_t)q;
+        L.mem[pos] = make_double2(xv[r], __longlong_as_double((int64_t)q));
       }
     }
     __syncthreads();
   }
+  GK_BMARK(5);
 
   // ---- the values: the rank inside a gap is the position minus the gap's
   //      member base when sorted, else the count of its members before it in
   //      (value, insertion index) order (gk:71-72); gk:93-99 for a gap before
   //      an entry, gk:85-92 for the tail: chunks of max(T,1), each emitting
   //      its last value
+  uint32_t pkv[GK_WG_VPT];
+  int rkv[GK_WG_VPT];
+#pragma unroll
+  for (int r = 0; r < GK_WG_VPT; ++r) {
+    const int q = t + GK_WG_T * r;
+    pkv[r] = q < cnt ? L.gpk[xg[r]] : 0u;
+    rkv[r] = q - (int)(pkv[r] >> 16);
+  }
+  if (!sorted) {
+    // both values' member lists walked side by side, one 16-byte read each
+    int mb[GK_WG_VPT], mn[GK_WG_VPT], nmax = 0;
+#pragma unroll
+    for (int r = 0; r < GK_WG_VPT; ++r) {
+      const int q = t + GK_WG_T * r;
+      mb[r] = (int)(pkv[r] >> 16);
+      mn[r] = q < cnt ? (xg[r] < E ? (int)(L.gpk[xg[r] + 1] >> 16) : totm) - mb[r] : 0;
+      nmax = max(nmax, mn[r]);
+      rkv[r] = 0;
+    }
+    // (GK_WG_RK_UNROLL members per value and trip: their reads are issued
+    // together, the compares masked past the value's own members)
+    for (int i = 0; i < nmax; i += GK_WG_RK_UNROLL) {
+      double2 e[GK_WG_VPT][GK_WG_RK_UNROLL];
+#pragma unroll
+      for (int r = 0; r < GK_WG_VPT; ++r)
+#pragma unroll
+        for (int u = 0; u < GK_WG_RK_UNROLL; ++u) e[r][u] = L.mem[min(mb[r] + i + u, GK_WG_PMAX - 1)];
+#pragma unroll
+      for (int r = 0; r < GK_WG_VPT; ++r) {
+        const double xq = xv[r];
+        const int q = t + GK_WG_T * r;
+#pragma unroll
+        for (int u = 0; u < GK_WG_RK_UNROLL; ++u)
+          rkv[r] += (i + u < mn[r] &&
+                     (e[r][u].x < xq || (!(xq < e[r][u].x) && (int)__double_as_longlong(e[r][u].y) < q))) ? 1 : 0;
+      }
+    }
+  }
 #pragma unroll
   for (int r = 0; r < GK_WG_VPT; ++r) {
     const int q = t + GK_WG_T * r;
     if (q < cnt) {
       const int gap = xg[r];
-      const uint32_t pk = L.gpk[gap];
-      int rk = q - (int)(pk >> 16);
-      if (!sorted) {
-        const int mb = (int)(pk >> 16);
-        const int me = gap < E ? (int)(L.gpk[gap + 1] >> 16) : totm;
-        const double xq = xv[r];
-        rk = 0;
-        for (int i = mb; i < me; ++i) {
-          const double u = L.sv[i];
-          rk += (u < xq || (!(xq < u) && L.si[i] < (uint32_t)q)) ? 1 : 0;
-        }
-      }
+      const uint32_t pk = pkv[r];
+      const int rk = rkv[r];
       if (gap < E) {
         const int k = L.gk[gap] & ~GK_KEEP_BIT;
         if (rk >= k) {
@@ -2140,6 +2194,7 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
   const int hi = gk_pow2_above(newE) - 1;
   for (int j = newE + t; j < hi; j += GK_WG_T) nv[j] = __longlong_as_double(0x7ff0000000000000LL);
   __syncthreads();
+  GK_BMARK(6);
   return newE;
 }
 
@@ -2157,6 +2212,12 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
   const int t = threadIdx.x;
   const int P = st.P;
   const int64_t K = *wg_count;
+#ifdef GK_PROF
+  if (t == 0) {
+    for (int i = 0; i < GK_PROF_NSEC; ++i) gk_big_prof().acc[i] = 0;
+    gk_big_prof().t = gk_cycles();
+  }
+#endif
   for (;;) {
     if (t == 0) item = (int64_t)atomicAdd(work, 1ull);
     __syncthreads();
@@ -2199,6 +2260,7 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
     // current flush); xn holds it
     double xn[GK_WG_VPT];
     bool have_next = false;
+    GK_BMARK(0);
     while (ok && used + need <= Lx) {
       const int cnt = p + (int)need;
       if (have_next) {
@@ -2228,6 +2290,7 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
           xn[r] = q < P ? (sb ? sb[P + q] : x[xo + used + need + q]) : 0.0;
         }
       }
+      GK_BMARK(1);
       const int nE = flush_wg(L, cur, E, xv, cnt, gk_threshold(st, n), t, sb != nullptr);
       if (nE < 0) {
         ok = false;
@@ -2240,6 +2303,7 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
       need = P;
       flushed = true;
       if (sb) sb += P;  // batch b at wso + b*P (k_presort)
+      GK_BMARK(7);
     }
     (void)flushed;
     if (ok) {
@@ -2289,7 +2353,12 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
       st.pend[s] = p;
     }
     __syncthreads();
+    GK_BMARK(9);
   }
+#ifdef GK_PROF
+  if (t == 0)
+    for (int i = 0; i < GK_PROF_NSEC; ++i) atomicAdd(&gk_prof_acc[i], gk_big_prof().acc[i]);
+#endif
 }
 
 // ===========================================================================
@@ -2939,6 +3008,227 @@ __device__ __forceinline__ void sort128_2(double (&a)[2], int lane) {
     a[1] = t1 ? p1 : a[1];
   }
   half_cleaners2<32>(a, lane);
+}
+
+// ===========================================================================
+// k_presort_reg (round 4): the presort of long streams' flush batches, one
+// WAVE per batch, in registers.  k_presort sorts a 1024-key batch with 256
+// threads through LDS (55 stages, two compare-exchanges per thread and stage
+// plus a barrier each): cfg5's 378k batches took 13.6 ms ahead of the
+// critical stream's ingest.  Here element e = lane*16 + r of the (padded)
+// batch lives in register a[r] of its lane; the bitonic network is run in the
+// form whose compare-exchanges always keep the minimum at the lower position
+// (a merge of two ascending runs of KB/2 = a mirror stage e ^ (KB-1), then
+// half-cleaners e ^ J): distances below 16 are inside a lane (one compare and
+// four selects per pair), 16 and up are lane exchanges on the VALU (DPP and
+// the permlane swaps of gk_xor.h).  Keys are values alone: equal values are
+// bit-identical, so their order cannot change a flush -- except +0.0 and
+// -0.0.  A batch holding both has its run of zeros rewritten after the sort
+// with the zeros' signs in insertion order (Python's stable sorted() of
+// gk:71-72 keeps equal keys in insertion order).
+// ===========================================================================
+#define GK_PS_R 16  // keys per lane (1024 per wave)
+
+template <bool KEYED>
+__device__ __forceinline__ bool ps_less(double a, uint32_t ia, double b, uint32_t ib) {
+  if constexpr (KEYED) return a < b || (!(b < a) && ia < ib);
+  else return a < b;
+}
+
+// intra-lane compare-exchange: position R1 (< R2) keeps the minimum
+template <bool KEYED>
+__device__ __forceinline__ void ps_ce(double& a1, double& a2, uint32_t& i1, uint32_t& i2) {
+  const bool sw = ps_less<KEYED>(a2, i2, a1, i1);
+  const double lo = sw ? a2 : a1, hi = sw ? a1 : a2;
+  a1 = lo;
+  a2 = hi;
+  if constexpr (KEYED) {
+    const uint32_t il = sw ? i2 : i1, ih = sw ? i1 : i2;
+    i1 = il;
+    i2 = ih;
+  }
+}
+
+// half-cleaners of distance J < 16 (inside every lane), J, J/2, .., 1
+template <bool KEYED, int J>
+__device__ __forceinline__ void ps_half_intra(double (&a)[GK_PS_R], uint32_t (&ix)[GK_PS_R]) {
+#pragma unroll
+  for (int r = 0; r < GK_PS_R; ++r)
+    if ((r & J) == 0) ps_ce<KEYED>(a[r], a[r | J], ix[r], ix[r | J]);
+  if constexpr (J > 1) ps_half_intra<KEYED, J / 2>(a, ix);
+}
+
+// merge of ascending runs of KB/2 into runs of KB, KB <= 16 (inside lanes)
+template <bool KEYED, int KB>
+__device__ __forceinline__ void ps_merge_intra(double (&a)[GK_PS_R], uint32_t (&ix)[GK_PS_R]) {
+#pragma unroll
+  for (int r = 0; r < GK_PS_R; ++r)
+    if ((r & (KB / 2)) == 0) ps_ce<KEYED>(a[r], a[r ^ (KB - 1)], ix[r], ix[r ^ (KB - 1)]);
+  if constexpr (KB >= 4) ps_half_intra<KEYED, KB / 4>(a, ix);
+}
+
+template <int M>
+__device__ __forceinline__ uint32_t ps_xor_u32(uint32_t v, int lane) { return (uint32_t)lane_xor_i32<M>((int)v, lane); }
+
+// half-cleaner of distance J >= 16: lanes l and l ^ (J/16), same r
+template <bool KEYED, int J>
+__device__ __forceinline__ void ps_half_cross(double (&a)[GK_PS_R], uint32_t (&ix)[GK_PS_R], int lane) {
+  constexpr int M = J / 16;
+  const bool lower = (lane & M) == 0;
+#pragma unroll
+  for (int r = 0; r < GK_PS_R; ++r) {
+    const double p = lane_xor_f64<M>(a[r], lane);
+    uint32_t ip = 0;
+    if constexpr (KEYED) ip = ps_xor_u32<M>(ix[r], lane);
+    const bool take = lower ? ps_less<KEYED>(p, ip, a[r], ix[r]) : ps_less<KEYED>(a[r], ix[r], p, ip);
+    a[r] = take ? p : a[r];
+    if constexpr (KEYED) ix[r] = take ? ip : ix[r];
+  }
+}
+
+// merge into runs of KB >= 32: the mirror stage pairs (l, r) with
+// (l ^ M, 15 - r), M = (KB - 1) / 16, then the half-cleaners
+template <bool KEYED, int KB>
+__device__ __forceinline__ void ps_merge_cross(double (&a)[GK_PS_R], uint32_t (&ix)[GK_PS_R], int lane) {
+  constexpr int M = (KB - 1) >> 4;
+  const bool lower = (lane & (KB / 32)) == 0;
+#pragma unroll
+  for (int r = 0; r < GK_PS_R / 2; ++r) {
+    const int r2 = GK_PS_R - 1 - r;
+    const double p1 = lane_xor_f64<M>(a[r2], lane), p2 = lane_xor_f64<M>(a[r], lane);
+    uint32_t i1 = 0, i2 = 0;
+    if constexpr (KEYED) {
+      i1 = ps_xor_u32<M>(ix[r2], lane);
+      i2 = ps_xor_u32<M>(ix[r], lane);
+    }
+    const bool t1 = lower ? ps_less<KEYED>(p1, i1, a[r], ix[r]) : ps_less<KEYED>(a[r], ix[r], p1, i1);
+    const bool t2 = lower ? ps_less<KEYED>(p2, i2, a[r2], ix[r2]) : ps_less<KEYED>(a[r2], ix[r2], p2, i2);
+    a[r] = t1 ? p1 : a[r];
+    a[r2] = t2 ? p2 : a[r2];
+    if constexpr (KEYED) {
+      ix[r] = t1 ? i1 : ix[r];
+      ix[r2] = t2 ? i2 : ix[r2];
+    }
+  }
+  if constexpr (KB / 4 >= 16) ps_half_cross<KEYED, KB / 4>(a, ix, lane);
+  if constexpr (KB / 8 >= 16) ps_half_cross<KEYED, KB / 8>(a, ix, lane);
+  if constexpr (KB / 16 >= 16) ps_half_cross<KEYED, KB / 16>(a, ix, lane);
+  if constexpr (KB / 32 >= 16) ps_half_cross<KEYED, KB / 32>(a, ix, lane);
+  if constexpr (KB / 64 >= 16) ps_half_cross<KEYED, KB / 64>(a, ix, lane);
+  ps_half_intra<KEYED, 8>(a, ix);
+}
+
+template <bool KEYED>
+__device__ __forceinline__ void ps_sort1024(double (&a)[GK_PS_R], uint32_t (&ix)[GK_PS_R], int lane) {
+  ps_merge_intra<KEYED, 2>(a, ix);
+  ps_merge_intra<KEYED, 4>(a, ix);
+  ps_merge_intra<KEYED, 8>(a, ix);
+  ps_merge_intra<KEYED, 16>(a, ix);
+  ps_merge_cross<KEYED, 32>(a, ix, lane);
+  ps_merge_cross<KEYED, 64>(a, ix, lane);
+  ps_merge_cross<KEYED, 128>(a, ix, lane);
+  ps_merge_cross<KEYED, 256>(a, ix, lane);
+  ps_merge_cross<KEYED, 512>(a, ix, lane);
+  ps_merge_cross<KEYED, 1024>(a, ix, lane);
+}
+
+__global__ __launch_bounds__(64) void k_presort_reg(GKState st, const double* __restrict__ x,
+                                                    const int64_t* __restrict__ offs,
+                                                    const int32_t* __restrict__ list,
+                                                    const int32_t* __restrict__ count,
+                                                    const int64_t* __restrict__ list_n,
+                                                    const int64_t* __restrict__ list_ws,
+                                                    const int64_t* __restrict__ list_b0, double* __restrict__ ws) {
+  __shared__ uint8_t zs[64 * GK_PS_R];
+  const int cnt = *count;
+  if (cnt <= 0) return;
+  const int64_t total = list_b0[cnt];
+  const int lane = threadIdx.x;
+  const int P = st.P;
+  // a contiguous range of global batches per wave (as k_presort)
+  const int64_t g0 = total * blockIdx.x / gridDim.x, g1 = total * (blockIdx.x + 1) / gridDim.x;
+  if (g0 >= g1) return;
+  int i = 0;
+  {
+    int lo = 0, hi = cnt - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (list_b0[mid] <= g0) lo = mid;
+      else hi = mid - 1;
+    }
+    i = lo;
+  }
+  int64_t bnext = i + 1 < cnt ? list_b0[i + 1] : INT64_MAX;
+  int ci = -1;
+  int64_t wso = -1, b0 = 0, s = 0, xo = 0, need = 0;
+  int p = 0;
+  for (int64_t gb = g0; gb < g1; ++gb) {
+    while (gb >= bnext) {
+      ++i;
+      bnext = i + 1 < cnt ? list_b0[i + 1] : INT64_MAX;
+    }
+    if (i != ci) {
+      ci = i;
+      wso = list_ws[i];
+      b0 = list_b0[i];
+      s = list[i];
+      xo = offs[s];
+      p = st.pend[s];
+      need = P - (list_n[i] % P);
+    }
+    if (wso < 0) continue;
+    const int64_t b = gb - b0;
+    const double* pb = st.pbuf + s * (int64_t)st.pmax;
+    const int m = b == 0 ? p + (int)need : P;
+    const int64_t xb = b == 0 ? xo : xo + need + (b - 1) * P;
+    double a[GK_PS_R];
+    uint32_t ix[GK_PS_R];
+    bool pz = false, nz = false;
+#pragma unroll
+    for (int r = 0; r < GK_PS_R; ++r) {
+      const int e = lane * GK_PS_R + r;
+      double v = __longlong_as_double(0x7ff0000000000000LL);
+      if (e < m) v = (b == 0 && e < p) ? pb[e] : x[xb + (b == 0 ? e - p : e)];
+      a[r] = v;
+      ix[r] = (uint32_t)e;
+      const bool z = e < m && v == 0.0;
+      pz |= z && !signbit(v);
+      nz |= z && signbit(v);
+    }
+    const bool mixed = __builtin_amdgcn_ballot_w64(pz) != 0 && __builtin_amdgcn_ballot_w64(nz) != 0;
+    int zneg = 0;  // values below zero (the zero run starts there after the sort)
+    if (mixed) {
+      // the zeros' signs by their rank among the zeros in insertion order
+      int zc = 0;
+#pragma unroll
+      for (int r = 0; r < GK_PS_R; ++r) {
+        const int e = lane * GK_PS_R + r;
+        zc += (e < m && a[r] == 0.0) ? 1 : 0;
+        zneg += (e < m && a[r] < 0.0) ? 1 : 0;
+      }
+      int zr = (int)wave_incl_scan_u32((uint32_t)zc, lane) - zc;
+#pragma unroll
+      for (int r = 0; r < GK_PS_R; ++r) {
+        const int e = lane * GK_PS_R + r;
+        if (e < m && a[r] == 0.0) zs[zr++] = signbit(a[r]) ? 1 : 0;
+      }
+      zneg = wave_sum_i32(zneg);
+      wsync<false>();
+    }
+    ps_sort1024<false>(a, ix, lane);
+    if (mixed) {
+#pragma unroll
+      for (int r = 0; r < GK_PS_R; ++r)
+        if (a[r] == 0.0) a[r] = zs[lane * GK_PS_R + r - zneg] ? -0.0 : 0.0;
+      wsync<false>();  // (zs is rewritten by the next batch)
+    }
+    double* out = ws + wso + b * P;
+#pragma unroll
+    for (int r = 0; r < GK_PS_R; ++r) {
+      const int e = lane * GK_PS_R + r;
+      if (e < m) out[e] = a[r];
+    }
+  }
 }
 
 // One flush of the small class; K entries per lane (E <= 64*K - 1).  Returns
@@ -4640,8 +4930,15 @@ hipError_t gk_launch_presort(const GKState& st, const double* x, const int64_t* 
                              const int64_t* long_n, const int32_t* long_count, const GKPresort& ps,
                              hipStream_t stream) {
   if (st.S <= 0 || !ps.list_ws || !ps.ws || ps.ws_cap <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_presort, dim3((unsigned)(num_cu() * 8)), dim3(256), 0, stream, st, x, offs, long_list,
-                     long_count, long_n, (const int64_t*)ps.list_ws, (const int64_t*)ps.list_b0, ps.ws);
+  // one wave per batch in registers (k_presort_reg, P <= 1024); GK_PRESORT_REG=0
+  // or larger batches: the LDS sort of k_presort
+  static const int reg = getenv("GK_PRESORT_REG") ? atoi(getenv("GK_PRESORT_REG")) : 1;
+  if (reg && st.P <= 64 * GK_PS_R)
+    hipLaunchKernelGGL(k_presort_reg, dim3((unsigned)(num_cu() * 16)), dim3(64), 0, stream, st, x, offs, long_list,
+                       long_count, long_n, (const int64_t*)ps.list_ws, (const int64_t*)ps.list_b0, ps.ws);
+  else
+    hipLaunchKernelGGL(k_presort, dim3((unsigned)(num_cu() * 8)), dim3(256), 0, stream, st, x, offs, long_list,
+                       long_count, long_n, (const int64_t*)ps.list_ws, (const int64_t*)ps.list_b0, ps.ws);
   return hipGetLastError();
 }
 

@@ -86,7 +86,7 @@ struct GKPresort {
   int64_t ws_cap = 0;
   int64_t* ws_need = nullptr;  // device, 1 value
   int32_t* wg_count = nullptr; // device, 1 value: k_ingest_wg's streams (the head of the long list); NULL: none
-  int wg_presort = 0;          // with wg_count: presort as without it (1) or nothing (0: k_ingest_wg ranks)
+  int wg_presort = 1;          // with wg_count: presort as without it (1) or nothing (0: k_ingest_wg ranks)
 };
 // one workgroup per stream for the first *wg_count streams of the long list
 // (class lcls = 0 of the 2048 class only); the prio k_ingest launch skips them

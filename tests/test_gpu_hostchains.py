@@ -10,7 +10,9 @@ starts from a non-trivial pre-call state), with signed zeros, infinities and
 a NaN in the host-walked streams, and with a fused quantile query (answered
 for the long streams after the host results are applied).
 
-Round 4: the host walk is asynchronous (a worker thread of the set, joined on
+Round 4: the host walk is off by default (GK_HOST_CHAINS=1 or
+GK_HOST_CHAIN_MIN turns it on): k_stats_long's speculative walk is faster.
+When on, it is asynchronous (a worker thread of the set, joined on
 the caller's stream by k_hc_wait): gk_ingest returns before the ingest kernel
 completes; the number of streams the host took is asserted; a
 failed host walk (GK_HC_FAIL=1 injects one) is walked on the device instead
@@ -123,12 +125,13 @@ def test_failed_host_walk_is_walked_on_the_device(gpu_device, monkeypatch):
 
 
 def test_ingest_with_host_chains_returns_before_the_kernel(gpu_device, monkeypatch):
-    """with a stream past the host-chain threshold (2^20
-    values, the default) in the batch, gk_ingest_quantiles only enqueues --
-    it returns while the ingest is still running on the device -- and the
-    joined results are exact."""
+    """with host chains on (GK_HOST_CHAINS=1; off by
+    default since the device walk became speculative) and a stream past their
+    threshold (2^20 values, the default) in the batch, gk_ingest_quantiles
+    only enqueues -- it returns while the ingest is still running on the
+    device -- and the joined results are exact."""
     monkeypatch.delenv("GK_HOST_CHAIN_MIN", raising=False)
-    monkeypatch.delenv("GK_HOST_CHAINS", raising=False)
+    monkeypatch.setenv("GK_HOST_CHAINS", "1")
     rng = np.random.default_rng(77)
     lens = rng.integers(1, 2000, 64)
     lens[0] = 3 << 20

@@ -25,6 +25,10 @@ SECTIONS = ["stream setup (header, table load)", "gap search", "counts (zero, at
             "pad + end of flush", "between flushes (T, next flush setup)", "leftover, quantiles, write-back",
             "next flush's values (prefetch wait)", "-"]
 
+SECTIONS_WG = ["stream setup + loop top", "batch load + next-batch prefetch", "gap search + counts",
+               "carry walk", "scan + per-gap bases + keeps", "member stores (unsorted)",
+               "rank + place + pad", "end of flush", "-", "write-back", "crowded-gap sort", "-"]
+
 SECTIONS_BIG = ["stream setup (header, table load)", "gap search", "counts (zero, atomics, max gap)",
                 "carry walk (rounds)", "sums + scan + keeps", "rank loop + emit", "bitonic sort + emit",
                 "pad + end of flush", "between flushes", "leftover, quantiles, write-back", "-", "-"]
@@ -32,22 +36,27 @@ SECTIONS_BIG = ["stream setup (header, table load)", "gap search", "counts (zero
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", default="cfg3", choices=["cfg3", "cfg2", "long"])
+    ap.add_argument("--workload", default="cfg3", choices=["cfg3", "cfg2", "long", "wg"])
     ap.add_argument("--streams", type=int, default=0)
     a = ap.parse_args()
     from bench import make_input
     from gkarray_amd import StreamSet
     S, L, dist_name = {"cfg3": (1_000_000, 1000, "pareto"), "cfg2": (100_000, 10_000, "lognormal"),
-                       "long": (64, 1_000_000, "lognormal")}[a.workload]
+                       "long": (64, 1_000_000, "lognormal"), "wg": (64, 1_000_000, "lognormal")}[a.workload]
     S = a.streams or S
     dev = torch.device("cuda", 0)
     x, offs = make_input(S, L, 3, dev, dist_name)
     # "long": eps=0.001 streams of 1M values in the 2048 class (k_ingest<2048>,
     # sections of flush_wave: SECTIONS_BIG)
-    eps = 0.001 if a.workload == "long" else 0.01
+    # "wg": the same streams through k_ingest_wg (GK_WG=1; GK_WG_PRESORT from
+    # the environment), sections of flush_wg: SECTIONS_WG
+    eps = 0.001 if a.workload in ("long", "wg") else 0.01
     global SECTIONS
     if a.workload == "long":
         SECTIONS = SECTIONS_BIG
+    if a.workload == "wg":
+        os.environ["GK_WG"] = "1"
+        SECTIONS = SECTIONS_WG
     ss = StreamSet(S, eps, device=dev)
     lib = ctypes.CDLL(os.environ["GK_LIB_PATH"])
     acc = (ctypes.c_ulonglong * 12)()
