@@ -1,7 +1,9 @@
 """Per-launch SQ counters of k_ingest_small from scripts/pmc_sq.sh output dirs,
-per flush (1e7 flushes per cfg3 launch) and LDS share.  Usage: sq_summary.py TAG [TAG2 ...]"""
+per flush (1e7 flushes per cfg3 launch) and LDS share.  Usage: sq_summary.py TAG [TAG2 ...]
+(KRX in the environment: another kernel name, e.g. k_ingest_half)"""
 import csv
 import glob
+import os
 import sys
 
 FLUSHES = 1e7
@@ -11,7 +13,7 @@ def load(tag):
     agg = {}
     for f in glob.glob("gpurun_out/%s_p*/**/*counter_collection.csv" % tag, recursive=True):
         for r in csv.DictReader(open(f)):
-            if "k_ingest_small" in r["Kernel_Name"]:
+            if os.environ.get("KRX", "k_ingest_small") in r["Kernel_Name"]:
                 agg.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     return {k: v[-1] for k, v in agg.items()}
 
