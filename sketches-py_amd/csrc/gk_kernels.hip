@@ -1920,6 +1920,9 @@ __device__ __forceinline__ void wg_sort(WgLDS& L, double (&xv)[GK_WG_VPT], int c
 #ifndef GK_WG_RK_UNROLL
 #define GK_WG_RK_UNROLL 4
 #endif
+#ifndef GK_WG_SEARCH8
+#define GK_WG_SEARCH8 0  // 8-ary rounds: measured no faster (r04n: search 2.31e8 vs 2.23e8 cycles, cfg5 49.7 vs 49.1-49.4 ms)
+#endif
 __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG_VPT], const int cnt,
                         const int T, const int t, bool sorted) {
   const int lane = t & 63, w = t >> 6;
@@ -1935,6 +1938,40 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
   for (;;) {
 #pragma unroll
     for (int r = 0; r < GK_WG_VPT; ++r) xg[r] = 0;
+#if GK_WG_SEARCH8
+    // 8-ary rounds (7 probes issued together: 4 dependent LDS round trips
+    // for a 1024-slot table instead of 10), then 4- / 2-ary for the rest
+    {
+      const int P2 = gk_pow2_above(E);
+      int bits = 31 - __builtin_clz(P2);  // log2(P2)
+      int step = P2;
+      while (bits >= 3) {
+        step >>= 3;
+        bits -= 3;
+        double tt[GK_WG_VPT][7];
+#pragma unroll
+        for (int r = 0; r < GK_WG_VPT; ++r)
+#pragma unroll
+          for (int k = 0; k < 7; ++k) tt[r][k] = tv[xg[r] + (k + 1) * step - 1];
+#pragma unroll
+        for (int r = 0; r < GK_WG_VPT; ++r) {
+          int c = 0;
+#pragma unroll
+          for (int k = 0; k < 7; ++k) c += (tt[r][k] <= xv[r]) ? 1 : 0;
+          xg[r] += c * step;
+        }
+      }
+      while (bits > 0) {
+        step >>= 1;
+        --bits;
+        double tt[GK_WG_VPT];
+#pragma unroll
+        for (int r = 0; r < GK_WG_VPT; ++r) tt[r] = tv[xg[r] + step - 1];
+#pragma unroll
+        for (int r = 0; r < GK_WG_VPT; ++r) xg[r] += (tt[r] <= xv[r]) ? step : 0;
+      }
+    }
+#else
     for (int step = gk_pow2_above(E) >> 1; step > 0; step >>= 1) {
       double tt[GK_WG_VPT];
 #pragma unroll
@@ -1942,6 +1979,7 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
 #pragma unroll
       for (int r = 0; r < GK_WG_VPT; ++r) xg[r] += (tt[r] <= xv[r]) ? step : 0;
     }
+#endif
 #pragma unroll
     for (int r = 0; r < GK_WG_VPT; ++r) xg[r] = min(xg[r], E);
     for (int j = t; j <= E; j += GK_WG_T) L.gpk[j] = 0u;
@@ -3234,10 +3272,24 @@ __global__ __launch_bounds__(64) void k_presort_reg(GKState st, const double* __
 // One flush of the small class; K entries per lane (E <= 64*K - 1).  Returns
 // the new table size, or -1 if it would exceed SMALL_CAP-1 (the table is then
 // untouched... except for the counts, which the caller discards).
+#ifndef GK_SORTALL
+#define GK_SORTALL 0
+#endif
 template <int VPL, int K, typename AfterSearch>
-__device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const double (&xv)[VPL], const int cnt,
+__device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const double (&xv_in)[VPL], const int cnt,
                                            const int T, const CsDiv cd, const int lane, AfterSearch&& after_search) {
   static_assert(K == 2, "the 128-entry class holds 2 entries per lane");
+#if GK_SORTALL
+  // (experiment, VERDICT r03 1(d): every flush's batch sorted in registers
+  // first, ranks = position - gap member base, no member stores / rank loop)
+  double xv[VPL];
+#pragma unroll
+  for (int r = 0; r < VPL; ++r) xv[r] = xv_in[r];
+  bool sorted_batch = false;
+#else
+  const double (&xv)[VPL] = xv_in;
+  constexpr bool sorted_batch = false;
+#endif
   // cd = make_csdiv(T): the chunk-size divider, made by the caller (for an
   // automatic flush one flush ahead, so that its magic-number scalar load is
   // not waited for on the flush's critical path)
@@ -3278,6 +3330,27 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
       }
     }
   }
+#if GK_SORTALL
+  if constexpr (VPL == 2) {
+    bool pz = false, nz = false;
+#pragma unroll
+    for (int r = 0; r < VPL; ++r) {
+      const bool z = (lane + 64 * r < cnt) && xv[r] == 0.0;
+      pz |= z && !signbit(xv[r]);
+      nz |= z && signbit(xv[r]);
+    }
+    if (!(__builtin_amdgcn_ballot_w64(pz) != 0 && __builtin_amdgcn_ballot_w64(nz) != 0)) {
+      double a[2];
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+        a[r] = (lane + 64 * r < cnt) ? xv[r] : __longlong_as_double(0x7ff0000000000000LL);
+      sort128_2(a, lane);
+      xv[0] = a[0];
+      xv[1] = a[1];
+      sorted_batch = true;
+    }
+  }
+#endif
   // ---- gap = #entries <= x (gk:93): 7 levels over the padded table ---------
   // (slots E .. E+63 hold +inf, small_pad).  xb: byte offset of the padded
   // slot of the gap's entry; x = +inf may step into the padding: clamped to
@@ -3483,7 +3556,16 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
   GK_MARK(L, 4);
 
   // ---- stable order inside each gap (gk:72), then emit --------------------
-  if (!use_sort) {
+  if (sorted_batch) {
+    // (GK_SORTALL) sorted: a gap's members are contiguous, rank = position -
+    // the gap's member base
+#pragma unroll
+    for (int r = 0; r < VPL; ++r) {
+      const int2 gv = *(const int2*)((const char*)L.gi + xb[r]);
+      small_emit(L, xb[r] < pE8, cd, xv[r], gv, lane + 64 * r - gi_mb(gv.x), lane + 64 * r < cnt);
+    }
+    GK_MARK(L, 5);
+  } else if (!use_sort) {
     // Members of a gap are stored in slot order (the atomic slot xs).  A
     // value's rank in its gap counts the members below it.  Fast pass:
     // strict counts over every member (self included: never below itself);
