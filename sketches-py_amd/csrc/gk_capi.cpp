@@ -131,6 +131,7 @@ struct gk_set {
   double* d_qs = nullptr;
   int qs_alloc = 0;
   hipEvent_t ev_qs = nullptr;  // the last H2D copy out of h_qs
+  int qs_n = 0;                // entries of the list last uploaded to d_qs (h_qs holds it)
   // eighths of a wave per CU of the small-class batch launch that walk the gk:52-59
   // stats chains first (0: separate k_stats launch); GK_FUSED_STATS overrides
   int fused_stats = 7;
@@ -162,6 +163,8 @@ struct gk_set {
   // k_presort of the long streams' flush batches runs here beside the short
   // streams' chains (k_stats on the caller's stream); the ingest waits for it
   hipStream_t aux2 = nullptr;
+  hipStream_t aux3 = nullptr;    // the presort when k_ingest_wg runs beside it (ps.done)
+  bool presort_active = false;   // a presort of this call not yet joined on the caller's stream
   hipEvent_t ev_presort = nullptr;
   hipEvent_t ev_wg = nullptr;  // k_ingest_wg (on aux2, after the presort) done
   bool wg_trace = false;       // GK_WG_TRACE=1 at creation: its stream count per completed call on stderr (tests)
@@ -415,6 +418,7 @@ int grow_pools(gk_set* h, hipStream_t s) {
     HIP_TRY(hipStreamSynchronize(s));
     HIP_TRY(hipStreamSynchronize(h->aux));
     if (h->aux2) HIP_TRY(hipStreamSynchronize(h->aux2));
+    if (h->aux3) HIP_TRY(hipStreamSynchronize(h->aux3));
     if (h->ps.ws) (void)hipFree(h->ps.ws);
     h->ps.ws = nullptr;
     h->ps.ws_cap = 0;
@@ -682,6 +686,8 @@ void hc_shutdown(gk_set* h) {
 // the device (k_hc_fallback with the fail word set).
 void stats_abort(gk_set* h, hipStream_t s) {
   if (h->forked) (void)hipStreamWaitEvent(s, h->ev_join, 0);
+  if (h->presort_active) (void)hipStreamWaitEvent(s, h->ev_presort, 0);
+  h->presort_active = false;
   if (h->hc_active) {
     const int32_t one = 1;
     if (hipMemcpyAsync(h->d_hc_fail, &one, sizeof(one), hipMemcpyHostToDevice, s) == hipSuccess)
@@ -735,9 +741,13 @@ int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s) {
   HIP_TRY(hipEventRecord(h->ev_join, h->aux));
   const bool presort = h->ps.list_ws && h->ps.ws && h->ps.ws_cap > 0;
   if (presort) {
-    HIP_TRY(hipStreamWaitEvent(h->aux2, h->ev_fork, 0));
-    HIP_TRY(gk_launch_presort(h->st, x, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->ps, h->aux2));
-    HIP_TRY(hipEventRecord(h->ev_presort, h->aux2));
+    // with k_ingest_wg beside it (ps.done): on its own stream, joined by
+    // stats_join; else on aux2 ahead of k_ingest_wg
+    hipStream_t ps_s = h->ps.done ? h->aux3 : h->aux2;
+    HIP_TRY(hipStreamWaitEvent(ps_s, h->ev_fork, 0));
+    HIP_TRY(gk_launch_presort(h->st, x, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->ps, ps_s));
+    HIP_TRY(hipEventRecord(h->ev_presort, ps_s));
+    h->presort_active = true;
   }
   if (!stats_fused(h)) HIP_TRY(gk_launch_stats_short(h->st, x, offs, s));
   // (with k_ingest_wg every presorted stream is one of its streams: the
@@ -753,6 +763,10 @@ int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s) {
 int stats_join(gk_set* h, hipStream_t s, const GKQuery& q) {
   h->forked = false;
   HIP_TRY(hipStreamWaitEvent(s, h->ev_join, 0));
+  if (h->presort_active) {
+    h->presort_active = false;
+    HIP_TRY(hipStreamWaitEvent(s, h->ev_presort, 0));
+  }
   if (h->hc_active) {
     h->hc_active = false;
     // hand the call to the worker (it walks while the GPU ingests) and join
@@ -1096,6 +1110,15 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
     if (wg) h->ps.wg_count = h->d_ctr + GK_CTR_WG;
     h->ps.wg_presort = 1;
     if (const char* e = getenv("GK_WG_PRESORT")) h->ps.wg_presort = atoi(e) != 0;
+    // the register presort beside k_ingest_wg (which takes presorted batches
+    // once it is done and ranks unsorted ones until then); GK_WG_CONC=0: the
+    // workgroups wait for the presort
+    bool conc = wg && h->ps.wg_presort && gk_presort_reg_grid(st) > 0;
+    if (const char* e = getenv("GK_WG_CONC")) conc = conc && atoi(e) != 0;
+    if (conc) {
+      h->ps.done = h->d_ctr + GK_CTR_PSDONE;
+      okm &= hipStreamCreateWithFlags(&h->aux3, hipStreamNonBlocking) == hipSuccess;
+    }
     h->wg_trace = getenv("GK_WG_TRACE") != nullptr;
     okm &= hipEventCreateWithFlags(&h->ev_wg, hipEventDisableTiming) == hipSuccess;
   }
@@ -1147,6 +1170,7 @@ int gk_destroy(gk_set* h) {
   for (hipEvent_t e : h->hc_ev) (void)hipEventDestroy(e);
   if (h->hc_copy) (void)hipStreamDestroy(h->hc_copy);
   if (h->aux2) (void)hipStreamDestroy(h->aux2);
+  if (h->aux3) (void)hipStreamDestroy(h->aux3);
   if (h->ev_presort) (void)hipEventDestroy(h->ev_presort);
   if (h->ev_wg) (void)hipEventDestroy(h->ev_wg);
   for (double* p : h->hc_buf) (void)hipHostFree(p);
@@ -1246,11 +1270,15 @@ static int prepare_query(gk_set* h, const double* qs, int nq, double* out, int m
         hipHostMalloc(&h->h_qs, cap * sizeof(double)) != hipSuccess)
       return fail(GK_E_NOMEM, "qs allocation failed");
     h->qs_alloc = cap;
+    h->qs_n = 0;
   }
-  if (nq) {
+  // (the same list as the last upload -- every step of a serving loop --
+  // is already on the device: no copy, no blit launch)
+  if (nq && !(nq == h->qs_n && memcmp(h->h_qs, qs, nq * sizeof(double)) == 0)) {
     memcpy(h->h_qs, qs, nq * sizeof(double));
     HIP_TRY(hipMemcpyAsync(h->d_qs, h->h_qs, nq * sizeof(double), hipMemcpyHostToDevice, s));
     HIP_TRY(hipEventRecord(h->ev_qs, s));
+    h->qs_n = nq;
   }
   q->qs = nq ? h->d_qs : nullptr;
   q->nq = nq;

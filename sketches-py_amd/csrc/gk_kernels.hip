@@ -1862,6 +1862,7 @@ struct WgLDS {
   uint32_t si[GK_WG_PMAX];
   double2 mem[GK_WG_PMAX];      // an unsorted batch's values by gap: (value, insertion index bits)
   uint32_t wsum[GK_WG_WAVES];   // the scan's wave totals
+  int psflag_pub[2];            // k_ingest_wg: the presort-done flag thread 0 saw, by flush parity
   int32_t xdone[GK_WG_WAVES], xc[GK_WG_WAVES];  // the carry walk's wave-boundary states
   uint32_t total;
 };
@@ -2244,10 +2245,20 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
                                                        int32_t* __restrict__ ovf_list,
                                                        unsigned long long* __restrict__ work,
                                                        const double* __restrict__ psort,
-                                                       const int64_t* __restrict__ prio_ws) {
+                                                       const int64_t* __restrict__ prio_ws,
+                                                       const int32_t* __restrict__ ps_done, int ps_grid) {
   __shared__ WgLDS L;
   __shared__ int64_t item;
+  // ps_done: the presort runs beside this launch; a presorted batch is used
+  // only once every presort wave has finished (seen by thread 0 with a
+  // relaxed load during one flush, published in LDS at its end, taken by all
+  // threads after the next flush's barriers with an acquire load of their
+  // own); before that batches are ranked unsorted.  Workgroup-uniform,
+  // monotone.
+  bool ps_ok = ps_done == nullptr;
+  int fk = 0;  // flushes of this workgroup (the LDS slot parity)
   const int t = threadIdx.x;
+  if (t == 0) L.psflag_pub[0] = L.psflag_pub[1] = 0;
   const int P = st.P;
   const int64_t K = *wg_count;
 #ifdef GK_PROF
@@ -2297,20 +2308,26 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
     // the next batch is loaded one flush ahead (its HBM latency under the
     // current flush); xn holds it
     double xn[GK_WG_VPT];
-    bool have_next = false;
+    bool have_next = false, next_sorted = false;
     GK_BMARK(0);
     while (ok && used + need <= Lx) {
       const int cnt = p + (int)need;
+      bool cur_sorted;
+      int pf = 0;
+      if (t == 0 && !ps_ok) pf = __hip_atomic_load(ps_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (have_next) {
 #pragma unroll
         for (int r = 0; r < GK_WG_VPT; ++r) xv[r] = xn[r];
-      } else if (sb) {
+        cur_sorted = next_sorted;
+      } else if (sb && ps_ok) {
+        cur_sorted = true;
 #pragma unroll
         for (int r = 0; r < GK_WG_VPT; ++r) {
           const int q = t + GK_WG_T * r;
           xv[r] = q < cnt ? sb[q] : 0.0;
         }
       } else {
+        cur_sorted = false;
 #pragma unroll
         for (int r = 0; r < GK_WG_VPT; ++r) {
           const int q = t + GK_WG_T * r;
@@ -2321,15 +2338,28 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
       // prefetch: the next automatic flush's batch (P values: presorted at
       // sb + P, or the call's next P values)
       have_next = used + need + P <= Lx;
+      next_sorted = sb != nullptr && ps_ok;
       if (have_next) {
 #pragma unroll
         for (int r = 0; r < GK_WG_VPT; ++r) {
           const int q = t + GK_WG_T * r;
-          xn[r] = q < P ? (sb ? sb[P + q] : x[xo + used + need + q]) : 0.0;
+          xn[r] = q < P ? (next_sorted ? sb[P + q] : x[xo + used + need + q]) : 0.0;
         }
       }
       GK_BMARK(1);
-      const int nE = flush_wg(L, cur, E, xv, cnt, gk_threshold(st, n), t, sb != nullptr);
+      const int nE = flush_wg(L, cur, E, xv, cnt, gk_threshold(st, n), t, cur_sorted);
+      if (!ps_ok) {
+        // the flag thread 0 saw at the start of the previous flush (published
+        // before this flush's barriers); this flush's reading for the next one
+        if (L.psflag_pub[fk & 1]) {
+          // (every thread's own acquire of the finished count: the presort's
+          // stores are visible to its later loads; the count only grows, so
+          // all threads agree)
+          ps_ok = __hip_atomic_load(ps_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= ps_grid;
+        }
+        if (t == 0) L.psflag_pub[(fk + 1) & 1] = pf >= ps_grid;
+      }
+      ++fk;
       if (nE < 0) {
         ok = false;
         break;
@@ -3170,18 +3200,38 @@ __device__ __forceinline__ void ps_sort1024(double (&a)[GK_PS_R], uint32_t (&ix)
   ps_merge_cross<KEYED, 1024>(a, ix, lane);
 }
 
+__device__ void presort_reg_range(const GKState& st, const double* __restrict__ x, const int64_t* __restrict__ offs,
+                                  const int32_t* __restrict__ list, const int cnt,
+                                  const int64_t* __restrict__ list_n, const int64_t* __restrict__ list_ws,
+                                  const int64_t* __restrict__ list_b0, double* __restrict__ ws, uint8_t* zs,
+                                  const int lane);
+
 __global__ __launch_bounds__(64) void k_presort_reg(GKState st, const double* __restrict__ x,
                                                     const int64_t* __restrict__ offs,
                                                     const int32_t* __restrict__ list,
                                                     const int32_t* __restrict__ count,
                                                     const int64_t* __restrict__ list_n,
                                                     const int64_t* __restrict__ list_ws,
-                                                    const int64_t* __restrict__ list_b0, double* __restrict__ ws) {
+                                                    const int64_t* __restrict__ list_b0, double* __restrict__ ws,
+                                                    int32_t* __restrict__ done) {
   __shared__ uint8_t zs[64 * GK_PS_R];
   const int cnt = *count;
-  if (cnt <= 0) return;
-  const int64_t total = list_b0[cnt];
   const int lane = threadIdx.x;
+  if (cnt > 0) presort_reg_range(st, x, offs, list, cnt, list_n, list_ws, list_b0, ws, zs, lane);
+  // (k_ingest_wg, running beside this launch, takes presorted batches once
+  // every wave has counted itself here: release of this wave's stores)
+  if (done) {
+    __threadfence();
+    if (lane == 0) atomicAdd(done, 1);
+  }
+}
+
+__device__ void presort_reg_range(const GKState& st, const double* __restrict__ x, const int64_t* __restrict__ offs,
+                                  const int32_t* __restrict__ list, const int cnt,
+                                  const int64_t* __restrict__ list_n, const int64_t* __restrict__ list_ws,
+                                  const int64_t* __restrict__ list_b0, double* __restrict__ ws, uint8_t* zs,
+                                  const int lane) {
+  const int64_t total = list_b0[cnt];
   const int P = st.P;
   // a contiguous range of global batches per wave (as k_presort)
   const int64_t g0 = total * blockIdx.x / gridDim.x, g1 = total * (blockIdx.x + 1) / gridDim.x;
@@ -4981,7 +5031,8 @@ hipError_t gk_launch_ingest_wg(const GKState& st, const double* x, const int64_t
   // (at most GK_WG_MAX streams: the count is only known on the device; the
   // spare workgroups find the hand-out exhausted and leave)
   hipLaunchKernelGGL(k_ingest_wg, dim3(GK_WG_MAX), dim3(GK_WG_T), 0, stream, st, x, offs, long_list, wg_count, lcls,
-                     force, ovf_count, ovf_list, work, (const double*)ps.ws, (const int64_t*)ps.list_ws);
+                     force, ovf_count, ovf_list, work, (const double*)ps.ws, (const int64_t*)ps.list_ws,
+                     (const int32_t*)ps.done, ps.done ? gk_presort_reg_grid(st) : 0);
   return hipGetLastError();
 }
 
@@ -5008,16 +5059,21 @@ hipError_t gk_launch_stats_short(const GKState& st, const double* x, const int64
   return hipGetLastError();
 }
 
+int gk_presort_reg_grid(const GKState& st) {
+  static const int reg = getenv("GK_PRESORT_REG") ? atoi(getenv("GK_PRESORT_REG")) : 1;
+  return (reg && st.P <= 64 * GK_PS_R) ? num_cu() * 16 : 0;
+}
+
 hipError_t gk_launch_presort(const GKState& st, const double* x, const int64_t* offs, const int32_t* long_list,
                              const int64_t* long_n, const int32_t* long_count, const GKPresort& ps,
                              hipStream_t stream) {
   if (st.S <= 0 || !ps.list_ws || !ps.ws || ps.ws_cap <= 0) return hipSuccess;
   // one wave per batch in registers (k_presort_reg, P <= 1024); GK_PRESORT_REG=0
   // or larger batches: the LDS sort of k_presort
-  static const int reg = getenv("GK_PRESORT_REG") ? atoi(getenv("GK_PRESORT_REG")) : 1;
-  if (reg && st.P <= 64 * GK_PS_R)
-    hipLaunchKernelGGL(k_presort_reg, dim3((unsigned)(num_cu() * 16)), dim3(64), 0, stream, st, x, offs, long_list,
-                       long_count, long_n, (const int64_t*)ps.list_ws, (const int64_t*)ps.list_b0, ps.ws);
+  if (gk_presort_reg_grid(st) > 0)
+    hipLaunchKernelGGL(k_presort_reg, dim3((unsigned)gk_presort_reg_grid(st)), dim3(64), 0, stream, st, x, offs,
+                       long_list, long_count, long_n, (const int64_t*)ps.list_ws, (const int64_t*)ps.list_b0, ps.ws,
+                       ps.done);
   else
     hipLaunchKernelGGL(k_presort, dim3((unsigned)(num_cu() * 8)), dim3(256), 0, stream, st, x, offs, long_list,
                        long_count, long_n, (const int64_t*)ps.list_ws, (const int64_t*)ps.list_b0, ps.ws);

@@ -87,6 +87,8 @@ struct GKPresort {
   int64_t* ws_need = nullptr;  // device, 1 value
   int32_t* wg_count = nullptr; // device, 1 value: k_ingest_wg's streams (the head of the long list); NULL: none
   int wg_presort = 1;          // with wg_count: presort as without it (1) or nothing (0: k_ingest_wg ranks)
+  int32_t* done = nullptr;     // device, 1 value: k_presort_reg's finished waves (k_ingest_wg runs beside
+                               // the presort and takes presorted batches once all are done); NULL: after it
 };
 // one workgroup per stream for the first *wg_count streams of the long list
 // (class lcls = 0 of the 2048 class only); the prio k_ingest launch skips them
@@ -100,6 +102,8 @@ hipError_t gk_launch_stats(const GKState& st, const int64_t* offs, int32_t* long
 // long ones are k_stats_long's), when class 0 is not the small class
 hipError_t gk_launch_stats_short(const GKState& st, const double* x, const int64_t* offs, hipStream_t stream);
 // k_presort over the plan k_long_prep wrote (no-op without a workspace)
+// k_presort_reg's grid (waves); k_ingest_wg compares *ps.done with it
+int gk_presort_reg_grid(const GKState& st);
 hipError_t gk_launch_presort(const GKState& st, const double* x, const int64_t* offs, const int32_t* long_list,
                              const int64_t* long_n, const int32_t* long_count, const GKPresort& ps,
                              hipStream_t stream);
@@ -176,6 +180,7 @@ hipError_t gk_launch_promote(const GKState& st, const int32_t* list, int64_t cou
 #define GK_CTR_OVFC 40    // [40 + round]
 #define GK_CTR_BADPEND 48 // gk_import: streams with an unreachable pending count
 #define GK_CTR_WG 50      // k_ingest_wg's stream count this call (k_long_prep)
+#define GK_CTR_PSDONE 51  // k_presort_reg's finished waves this call (k_ingest_wg beside it)
 #define GK_CTR_WORDS 16
 #define GK_CTR_CALL 14
 #define GK_CALL_WORK 256                          // bytes: the small-class launch's GK_WORK_BYTES, then
