@@ -259,3 +259,31 @@ def test_import_rejects_unreachable_pending(gpu_device):
     with pytest.raises(GKBackendError, match="pending"):
         ss.import_state(bad)
     assert_same_state(ss, o, "untouched after the refused import")
+
+
+def test_reset_after_deferring_call_does_not_wait_or_replay(gpu_device, monkeypatch):
+    """Round 4: reset() no longer waits for the previous call -- the streams
+    that call deferred are reset too, so its re-run is voided (never replayed
+    onto the reset state) -- while the deferrals of the call after the reset
+    are still re-run.  Three async calls with resets between them, 2 arena
+    slots (most overflowing streams deferred): the state equals an oracle that
+    saw only the last batch."""
+    monkeypatch.setenv("GK_POOL_SLOTS", "2")
+    rng = np.random.default_rng(87)
+    S = 48
+    ss = _ss(S, 0.01, gpu_device)
+    keep = []
+    for part in range(3):
+        flat, offs = _deferring_batch(S, rng)
+        tf, to = torch.from_numpy(flat).to(gpu_device), torch.from_numpy(offs).to(gpu_device)
+        keep.append((tf, to))
+        if part:
+            ss.reset()
+        q = ss.ingest(tf, to, quantiles=[0.25, 0.5, 0.99], sync=False)
+    ss.sync()
+    o = OracleSet(S, 0.01)
+    o.ingest(flat, offs)
+    assert ss.num_promoted > 2
+    assert_same_state(ss, o, "after reset + deferring call")
+    assert_same_quantiles(q.cpu().numpy(), o.quantiles([0.25, 0.5, 0.99]), "fused q after reset",
+                          small_of(o, 0.01))
