@@ -1855,7 +1855,7 @@ struct WgLDS {
   double tv[2][GK_WG_CAP];
   int32_t tg[2][GK_WG_CAP];
   int32_t td[2][GK_WG_CAP];
-  uint32_t gpk[GK_WG_CAP + 1];  // per gap: count, then (member base << 16) | out base
+  uint32_t gpk[2][GK_WG_CAP + 1];  // per gap: count, then (member base << 16) | out base; by table parity
   int32_t gk[GK_WG_CAP + 1];    // per entry: absorbed count | KEEP bit
   int32_t gdel[GK_WG_CAP + 1];  // per entry: G, then G + d - 1
   double sv[GK_WG_PMAX];        // sort area of a batch with a crowded gap
@@ -1933,10 +1933,18 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
   double* __restrict__ nv = L.tv[cur ^ 1];
   int32_t* __restrict__ ng = L.tg[cur ^ 1];
   int32_t* __restrict__ nd = L.td[cur ^ 1];
+  // per-gap counts / bases: two buffers by table parity; this flush's was
+  // zeroed during the previous one (or at stream setup), the other is zeroed
+  // now for the next flush (no zeroing pass + barrier before the atomics)
+  uint32_t* __restrict__ gpk = L.gpk[cur];
+  {
+    uint32_t* __restrict__ gz = L.gpk[cur ^ 1];
+    for (int j = t; j <= GK_WG_CAP; j += GK_WG_T) gz[j] = 0u;
+  }
   // ---- gap = #entries <= x (gk:93), branch-free over the +inf-padded table
   int xg[GK_WG_VPT];
   uint32_t slot[GK_WG_VPT];  // an unsorted value's member slot in its gap
-  for (;;) {
+  for (int pass = 0;; ++pass) {
 #pragma unroll
     for (int r = 0; r < GK_WG_VPT; ++r) xg[r] = 0;
 #if GK_WG_SEARCH8
@@ -1983,14 +1991,16 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
 #endif
 #pragma unroll
     for (int r = 0; r < GK_WG_VPT; ++r) xg[r] = min(xg[r], E);
-    for (int j = t; j <= E; j += GK_WG_T) L.gpk[j] = 0u;
-    __syncthreads();
+    if (pass > 0) {  // (the re-search of a sorted batch: counts start over)
+      for (int j = t; j <= E; j += GK_WG_T) gpk[j] = 0u;
+      __syncthreads();
+    }
     bool big = false;
 #pragma unroll
     for (int r = 0; r < GK_WG_VPT; ++r) {
       slot[r] = 0;
       if (t + GK_WG_T * r < cnt) {
-        slot[r] = atomicAdd(&L.gpk[xg[r]], 1u);
+        slot[r] = atomicAdd(&gpk[xg[r]], 1u);
         big |= slot[r] >= GK_WG_RANK_MAX;
       }
     }
@@ -2029,7 +2039,7 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
     const bool in = k < nk;
     eg[k] = in ? tg[j0 + k] : 0;
     ed[k] = in ? td[j0 + k] : 0;
-    em[k] = in ? (int)L.gpk[j0 + k] : 0;
+    em[k] = in ? (int)gpk[j0 + k] : 0;
   }
   // the entry after this thread's block (the last entry's removal test)
   const bool nx = has && jend < E;
@@ -2037,7 +2047,7 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
   bool known = (t == 0) || !has;
   if (has && t > 0) {
     const int jp = j0 - 1;
-    const int g = tg[jp], d = td[jp], m = (int)L.gpk[jp];
+    const int g = tg[jp], d = td[jp], m = (int)gpk[jp];
     const int G0 = g + clampi(T - d - g, 0, m);
     known = !(G0 + eg[0] + ed[0] <= T);
   }
@@ -2081,12 +2091,13 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
       L.xdone[w] = done ? 1 : 0;
       L.xc[w] = cout;
     }
-    __syncthreads();
+    // (one barrier when no chain crosses a wave boundary: the common case)
+    if (__syncthreads_and(done ? 1 : 0)) break;
     if (lane == 0 && w > 0 && !known && L.xdone[w - 1]) {
       known = true;
       cin = L.xc[w - 1];
     }
-    if (__syncthreads_and(done ? 1 : 0)) break;
+    __syncthreads();  // (xdone / xc are rewritten by the next round)
   }
   GK_BMARK(3);
 
@@ -2101,7 +2112,7 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
     }
   }
   if (t == tail_t) {
-    const int mE = (int)L.gpk[E];
+    const int mE = (int)gpk[E];
     sm += (uint32_t)mE;
     so += (uint32_t)((mE + cs - 1) / cs);
   }
@@ -2129,7 +2140,7 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
         const int ka = kk & ~GK_KEEP_BIT;
         const int G = eG[k];
         const int d = ed[k];
-        L.gpk[j] = base;
+        gpk[j] = base;
         L.gk[j] = kk;
         L.gdel[j] = G + d - 1;
         if (kk & GK_KEEP_BIT) {
@@ -2141,7 +2152,7 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
         base += ((uint32_t)m << 16) | (uint32_t)(m - ka + ((kk & GK_KEEP_BIT) ? 1 : 0));
       }
     }
-    if (t == tail_t) L.gpk[E] = base;
+    if (t == tail_t) gpk[E] = base;
   }
   __syncthreads();
   GK_BMARK(4);
@@ -2150,7 +2161,7 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
     for (int r = 0; r < GK_WG_VPT; ++r) {
       const int q = t + GK_WG_T * r;
       if (q < cnt) {
-        const int pos = (int)(L.gpk[xg[r]] >> 16) + (int)slot[r];
+        const int pos = (int)(gpk[xg[r]] >> 16) + (int)slot[r];
         L.mem[pos] = make_double2(xv[r], __longlong_as_double((int64_t)q));
       }
     }
@@ -2168,7 +2179,7 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
 #pragma unroll
   for (int r = 0; r < GK_WG_VPT; ++r) {
     const int q = t + GK_WG_T * r;
-    pkv[r] = q < cnt ? L.gpk[xg[r]] : 0u;
+    pkv[r] = q < cnt ? gpk[xg[r]] : 0u;
     rkv[r] = q - (int)(pkv[r] >> 16);
   }
   if (!sorted) {
@@ -2178,7 +2189,7 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
     for (int r = 0; r < GK_WG_VPT; ++r) {
       const int q = t + GK_WG_T * r;
       mb[r] = (int)(pkv[r] >> 16);
-      mn[r] = q < cnt ? (xg[r] < E ? (int)(L.gpk[xg[r] + 1] >> 16) : totm) - mb[r] : 0;
+      mn[r] = q < cnt ? (xg[r] < E ? (int)(gpk[xg[r] + 1] >> 16) : totm) - mb[r] : 0;
       nmax = max(nmax, mn[r]);
       rkv[r] = 0;
     }
@@ -2297,6 +2308,7 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
       }
       const int hi = gk_pow2_above(E) - 1;
       for (int j = E + t; j < hi; j += GK_WG_T) L.tv[0][j] = __longlong_as_double(0x7ff0000000000000LL);
+      for (int j = t; j <= GK_WG_CAP; j += GK_WG_T) L.gpk[0][j] = 0u;  // (flush_wg zeroes the other)
     }
     __syncthreads();
     int64_t used = 0;
