@@ -1941,6 +1941,27 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
     uint32_t* __restrict__ gz = L.gpk[cur ^ 1];
     for (int j = t; j <= GK_WG_CAP; j += GK_WG_T) gz[j] = 0u;
   }
+  // this thread's block of entries for the carry walk below: their g, d (and
+  // those of the entries either side) read now, under the search; only the
+  // member counts wait for the atomics
+  constexpr int KM = GK_WG_KMAX;
+  const int K = (E + GK_WG_T - 1) / GK_WG_T;
+  const int j0 = t * K;
+  const int jend = min(j0 + K, E);
+  const int nk = max(jend - j0, 0);
+  const bool has = j0 < E;
+  const int cs = T > 1 ? T : 1;
+  const int tail_t = E == 0 ? 0 : (E - 1) / K;
+  int eg[KM], ed[KM];
+#pragma unroll
+  for (int k = 0; k < KM; ++k) {
+    const bool in = k < nk;
+    eg[k] = in ? tg[j0 + k] : 0;
+    ed[k] = in ? td[j0 + k] : 0;
+  }
+  const bool nx = has && jend < E;  // the entry after this block (the last entry's removal test)
+  const int gnx = nx ? tg[jend] : 0, dnx = nx ? td[jend] : 0;
+  const int gp_ = (has && t > 0) ? tg[j0 - 1] : 0, dp_ = (has && t > 0) ? td[j0 - 1] : 0;  // the entry before
   // ---- gap = #entries <= x (gk:93), branch-free over the +inf-padded table
   int xg[GK_WG_VPT];
   uint32_t slot[GK_WG_VPT];  // an unsorted value's member slot in its gap
@@ -2025,30 +2046,13 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
   // waits for its left neighbour: inside a wave over DPP, across waves through
   // LDS (one barrier per round; rounds are the longest chain of removed
   // entries crossing a wave boundary, usually none)
-  constexpr int KM = GK_WG_KMAX;
-  const int K = (E + GK_WG_T - 1) / GK_WG_T;
-  const int j0 = t * K;
-  const int jend = min(j0 + K, E);
-  const int nk = max(jend - j0, 0);
-  const bool has = j0 < E;
-  const int cs = T > 1 ? T : 1;
-  const int tail_t = E == 0 ? 0 : (E - 1) / K;
-  int eg[KM], ed[KM], em[KM];
+  int em[KM];
 #pragma unroll
-  for (int k = 0; k < KM; ++k) {
-    const bool in = k < nk;
-    eg[k] = in ? tg[j0 + k] : 0;
-    ed[k] = in ? td[j0 + k] : 0;
-    em[k] = in ? (int)gpk[j0 + k] : 0;
-  }
-  // the entry after this thread's block (the last entry's removal test)
-  const bool nx = has && jend < E;
-  const int gnx = nx ? tg[jend] : 0, dnx = nx ? td[jend] : 0;
+  for (int k = 0; k < KM; ++k) em[k] = k < nk ? (int)gpk[j0 + k] : 0;
   bool known = (t == 0) || !has;
   if (has && t > 0) {
-    const int jp = j0 - 1;
-    const int g = tg[jp], d = td[jp], m = (int)gpk[jp];
-    const int G0 = g + clampi(T - d - g, 0, m);
+    const int m = (int)gpk[j0 - 1];
+    const int G0 = gp_ + clampi(T - dp_ - gp_, 0, m);
     known = !(G0 + eg[0] + ed[0] <= T);
   }
   bool done = !has;
