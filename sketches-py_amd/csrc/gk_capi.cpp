@@ -92,10 +92,6 @@ struct gk_set {
   int32_t* h_ctr = nullptr;  // pinned: the counters as of the end of the last call
   hipEvent_t ev_done = nullptr;
   bool done_pending = false;
-  // calls are numbered (mark_done); a reset voids the deferrals of the calls
-  // before it (their streams are reset: nothing to re-run), so it need not
-  // wait for them
-  uint64_t call_seq = 0, done_seq = 0, void_seq = 0;
   // the last ingest / flush call: its inputs, kept to re-run deferred streams
   // (the caller keeps them valid until the set's next call or gk_sync)
   struct {
@@ -286,7 +282,6 @@ void poll(gk_set* h, bool block) {
     return;
   }
   h->done_pending = false;
-  if (h->done_seq <= h->void_seq) h->h_ctr[GK_CTR_DEFER] = 0;  // (a call before a reset: nothing to re-run)
   if (h->ps.wg_count && h->wg_trace && h->h_ctr[GK_CTR_WORDS] > 0)
     fprintf(stderr, "[gk] k_ingest_wg: %d stream(s)\n", h->h_ctr[GK_CTR_WORDS]);
   const int32_t fatal = h->h_ctr[GK_CTR_FATAL];
@@ -454,7 +449,6 @@ int mark_done(gk_set* h, hipStream_t s) {
     HIP_TRY(hipMemcpyAsync(h->h_ctr + GK_CTR_WORDS, h->ps.wg_count, sizeof(int32_t), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipEventRecord(h->ev_done, s));
   h->done_pending = true;
-  h->done_seq = ++h->call_seq;
   return GK_OK;
 }
 
@@ -1192,13 +1186,8 @@ int gk_reset(gk_set* h, void* stream) {
   int rc = check_set(h);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
-  // No wait for the last call: streams it may have deferred are reset here
-  // (nothing of that call is re-run later: its deferrals are voided), so a
-  // reset + ingest loop never blocks on the host.  The host walk of the last
-  // call reads its inputs: drained first.
-  hc_drain(h);
-  h->void_seq = h->call_seq;
-  h->last.may_defer = false;
+  rc = settle(h, s, false);  // a deferred re-run of the last call must not land after the reset
+  if (rc) return rc;
   // (k_reset puts every stream back in class 0: cls = slot = 0)
   // slots, member lists and re-run lists start over (FATAL stays cumulative:
   // a readback still in flight carries it)

@@ -262,12 +262,13 @@ def test_import_rejects_unreachable_pending(gpu_device):
 
 
 def test_reset_after_deferring_call_does_not_wait_or_replay(gpu_device, monkeypatch):
-    """Round 4: reset() no longer waits for the previous call -- the streams
-    that call deferred are reset too, so its re-run is voided (never replayed
-    onto the reset state) -- while the deferrals of the call after the reset
-    are still re-run.  Three async calls with resets between them, 2 arena
-    slots (most overflowing streams deferred): the state equals an oracle that
-    saw only the last batch."""
+    """reset() right after an asynchronous call that deferred streams, then
+    another deferring call: the first call's deferred re-run must not land
+    after the reset, the last call's deferrals are re-run.  Three async calls
+    with resets between them, 2 arena slots (most overflowing streams
+    deferred): the state equals an oracle that saw only the last batch.  (A
+    reset that skipped the wait and voided the earlier deferrals was tried in
+    round 4 and failed this test: reverted.)"""
     monkeypatch.setenv("GK_POOL_SLOTS", "2")
     rng = np.random.default_rng(87)
     S = 48
