@@ -266,9 +266,7 @@ def test_reset_after_deferring_call_does_not_wait_or_replay(gpu_device, monkeypa
     another deferring call: the first call's deferred re-run must not land
     after the reset, the last call's deferrals are re-run.  Three async calls
     with resets between them, 2 arena slots (most overflowing streams
-    deferred): the state equals an oracle that saw only the last batch.  (A
-    reset that skipped the wait and voided the earlier deferrals was tried in
-    round 4 and failed this test: reverted.)"""
+    deferred): the state equals an oracle that saw only the last batch."""
     monkeypatch.setenv("GK_POOL_SLOTS", "2")
     rng = np.random.default_rng(87)
     S = 48
@@ -284,7 +282,8 @@ def test_reset_after_deferring_call_does_not_wait_or_replay(gpu_device, monkeypa
     ss.sync()
     o = OracleSet(S, 0.01)
     o.ingest(flat, offs)
-    assert ss.num_promoted > 2
-    assert_same_state(ss, o, "after reset + deferring call")
+    # (the fused query flushes the pending values: the oracle's quantiles() too)
     assert_same_quantiles(q.cpu().numpy(), o.quantiles([0.25, 0.5, 0.99]), "fused q after reset",
                           small_of(o, 0.01))
+    assert ss.num_promoted > 2
+    assert_same_state(ss, o, "after reset + deferring call")
