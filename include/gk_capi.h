@@ -21,9 +21,11 @@
  *    re-run by the device itself.  Part of an ingest (the sequential
  *    _sum/_avg chains of streams longer than 16384 values) runs on a stream
  *    the set owns; `stream` is made to wait for it, so every later call
- *    enqueued on `stream` sees the finished state.  The chains of the few
- *    longest streams (>= 2^20 values) are walked on host cores by a worker
- *    thread of the set: the call only hands them over (it does not block)
+ *    enqueued on `stream` sees the finished state.  Optionally
+ *    (GK_HOST_CHAINS=1 or GK_HOST_CHAIN_MIN in the environment; off by
+ *    default) the chains of the few longest streams (>= 2^20 values) are
+ *    walked on host cores by a worker thread of the set: the call only
+ *    hands them over (it does not block)
  *    and `stream` waits for the worker on the device (a kernel polling a
  *    pinned flag, bounded at 20 s; a failed host walk is redone on the
  *    device, same bits).  The set's next call, gk_sync and gk_destroy first
