@@ -21,8 +21,8 @@ the batch's values / max-over-ranks time.  The weak line (every rank its own
 1M streams, seed + rank) is measured in the same run and reported beside it
 under "weak" (``--split weak`` makes it the headline; ``--no-weak`` skips it).
 
-    python bench.py [--gpus N --steps K --warmup W]
-    torchrun --nproc-per-node N bench.py --gpus N ...
+    python bench.py [--gpus N --steps K --warmup W]   (N > 1: starts N ranks itself)
+    torchrun --nproc-per-node N bench.py --gpus N ...  (--gpus must equal the world size)
 """
 import argparse
 import json
@@ -266,15 +266,45 @@ def rank_streams(workload, offs, world, rank):
     return torch.arange(a, b, dtype=torch.int64)
 
 
+def free_port():
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` (N > 1) outside a torchrun environment: start the N
+    ranks as ONE child launcher (torch.distributed.run, one process per GPU,
+    rendezvous on 127.0.0.1) and return its exit code.  This process has made
+    no GPU call (only torch.cuda.device_count(), which does not initialise the
+    device) and is not replaced: the ranks are children; rank 0 prints the
+    line."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % n,
+           "--master-addr=127.0.0.1", "--master-port=%d" % free_port(), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     on_gpu = a.device == "cuda"
     # GK_BENCH_REHEARSE=1: rehearse the N-rank path on fewer GPUs (ranks share
     # devices, gloo for the timing collectives; the numbers mean nothing)
     rehearse = os.environ.get("GK_BENCH_REHEARSE") == "1" or not on_gpu
+    if a.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if on_gpu and not rehearse and a.gpus > torch.cuda.device_count():
+        sys.exit("bench.py: --gpus %d but this node has %d GPU(s) (GK_BENCH_REHEARSE=1 shares them)"
+                 % (a.gpus, torch.cuda.device_count()))
+    if "WORLD_SIZE" not in os.environ:
+        if a.gpus > 1:
+            sys.exit(launch_ranks(a.gpus))
+    elif int(os.environ["WORLD_SIZE"]) != a.gpus:
+        sys.exit("bench.py: --gpus %d but the launcher started %s rank(s)" % (a.gpus, os.environ["WORLD_SIZE"]))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
     if on_gpu:
         if rehearse:
             local %= max(torch.cuda.device_count(), 1)

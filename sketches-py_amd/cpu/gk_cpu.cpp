@@ -561,13 +561,16 @@ int gk_merge(gk_set* dst, gk_set* const* srcs, int nsrcs, void* stream) {
   if (nsrcs < 0 || (nsrcs > 0 && !srcs)) return fail(GK_E_ARG, "bad source list");
   for (int k = 0; k < nsrcs; ++k) {
     if (!srcs[k]) return fail(GK_E_ARG, "null source %d", k);
-    if (srcs[k] == dst) return fail(GK_E_ARG, "a set cannot be merged into itself");
     if (srcs[k]->eps != dst->eps)  // gk:118-119
       return fail(GK_E_EPS_MISMATCH, "Cannot merge two GKArrays with different epsilon values");
     if (srcs[k]->S != dst->S)
       return fail(GK_E_ARG, "stream counts differ (%lld vs %lld)", (long long)srcs[k]->S, (long long)dst->S);
   }
   // the fold runs per stream: dst.merge(srcs[0]); dst.merge(srcs[1]); ...
+  // A source may be dst itself (gk:111-154 accepts other is self: the flush
+  // of gk:137 empties dst's own incoming, the conversion reads the flushed
+  // table into `conv` before gk:154 rewrites it, gk:149 doubles n) or repeat
+  // (flushed again at each merge, as the reference does).
   parallel_for(dst->S, dst->threads, [&](int64_t s) {
     std::vector<Rec> conv;
     for (int k = 0; k < nsrcs; ++k) merge_stream(dst, dst->st[s], srcs[k]->st[s], conv);

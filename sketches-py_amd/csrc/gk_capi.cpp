@@ -137,6 +137,7 @@ struct gk_set {
   int fused_stats = 7;
   // gk_fold_packed: receives the packed states merged into this set (made on first use)
   gk_set* fold_scratch = nullptr;
+  gk_set* self_scratch = nullptr;  // snapshot source of dst.merge(dst), made on first use
   // Host-walked chains: the gk:52-59 chains of the
   // longest streams run on host cores beside the GPU ingest.  hc_min: shortest
   // stream taken (0: off; GK_HOST_CHAINS=0 / GK_HOST_CHAIN_MIN); hc_threads:
@@ -1150,6 +1151,7 @@ int gk_destroy(gk_set* h) {
   hc_shutdown(h);  // the worker finishes its handed-out walks (their joins may be waiting on the device)
   (void)hipDeviceSynchronize();  // launches of this set may still be running on the caller's stream
   if (h->fold_scratch) gk_destroy(h->fold_scratch);
+  if (h->self_scratch) gk_destroy(h->self_scratch);
   GKState& st = h->st;
   void* ptrs[] = {st.n,       st.E,          st.pend,        st.mn,          st.mx,          st.sum,
                   st.avg,     st.cls,        st.slot,        st.pbuf,        h->d_qs,
@@ -1358,13 +1360,14 @@ int gk_stats(gk_set* h, int64_t* n, double* mn, double* mx, double* sum, double*
   return GK_OK;
 }
 
+static int merge_self(gk_set* dst, hipStream_t s, void* stream);
+
 int gk_merge(gk_set* dst, gk_set* const* srcs, int nsrcs, void* stream) {
   int rc = check_set(dst);
   if (rc) return rc;
   if (nsrcs < 0 || (nsrcs > 0 && !srcs)) return fail(GK_E_ARG, "bad source list");
   for (int k = 0; k < nsrcs; ++k) {
     if (!srcs[k]) return fail(GK_E_ARG, "null source %d", k);
-    if (srcs[k] == dst) return fail(GK_E_ARG, "a set cannot be merged into itself");
     if (srcs[k]->eps != dst->eps)  // gk:118-119
       return fail(GK_E_EPS_MISMATCH, "Cannot merge two GKArrays with different epsilon values");
     if (srcs[k]->S != dst->S)
@@ -1375,6 +1378,12 @@ int gk_merge(gk_set* dst, gk_set* const* srcs, int nsrcs, void* stream) {
   if (rc) return rc;
   for (int k = 0; k < nsrcs; ++k) {
     gk_set* src = srcs[k];
+    if (src == dst) {  // dst.merge(dst): the reference accepts it (gk:111-154)
+      rc = merge_self(dst, s, stream);
+      if (rc) return rc;
+      continue;
+    }
+    // a repeated source is flushed again at each of its merges (gk:137)
     rc = gk_sync(src, stream);
     if (rc) return rc;
     // other.merge_compress() -- unconditional in the reference (gk:126, 137)
@@ -1676,6 +1685,42 @@ int gk_pack(gk_set* h, void* buf, int64_t bytes, void* stream) {
   std::string err;
   rc = gkpack::pack<DevMem>(h, h->d_ovfl[1], h->d_ovfl[2], buf, bytes, stream, err);
   return (rc && !err.empty()) ? fail(rc, "%s", err.c_str()) : rc;
+}
+
+// dst.merge(dst), gk:111-154 with `other` IS self: gk:137 flushes dst itself
+// (emptying its incoming), gk:138-147 convert that flushed table, gk:149
+// doubles n, and gk:154 merges the converted records back.  k_merge reads the
+// source table while it rewrites the destination's, so the source is a
+// snapshot of the flushed dst: packed into a device buffer and imported into
+// a scratch set that is NOT flushed again (a second compress at the same
+// threshold is not a no-op).  Its pending count is 0 and its n equals dst's,
+// so k_merge takes the general branch (n > 0) or, for an empty stream, the
+// "other empty" branch whose flush of an empty stream changes nothing.
+static int merge_self(gk_set* dst, hipStream_t s, void* stream) {
+  int rc = gk_sync(dst, stream);
+  if (!rc) rc = begin_call(dst, s);
+  if (!rc) rc = run_ingest(dst, nullptr, nullptr, 2, s);  // other.merge_compress() (gk:137)
+  if (!rc) rc = mark_done(dst, s);
+  if (!rc) rc = gk_sync(dst, stream);
+  if (rc) return rc;
+  int64_t bytes = 0;
+  rc = gk_pack_bytes(dst, &bytes, stream);
+  if (rc) return rc;
+  DevBuf buf;
+  if (!buf.alloc((size_t)bytes)) return fail(GK_E_NOMEM, "self-merge: snapshot of %lld bytes", (long long)bytes);
+  rc = gk_pack(dst, buf.p, bytes, stream);
+  if (!rc && !dst->self_scratch) rc = gk_create(dst->S, dst->eps, 0, dst->device, &dst->self_scratch);
+  if (rc) return rc;
+  std::string err;
+  gkpack::Header hd{};
+  rc = gkpack::read_header<DevMem>(dst->self_scratch, buf.p, &hd, stream, err);
+  if (!rc) rc = gkpack::import_packed<DevMem>(dst->self_scratch, buf.p, hd, stream);
+  if (!rc) rc = gk_sync(dst->self_scratch, stream);
+  if (rc) return (!err.empty()) ? fail(rc, "%s", err.c_str()) : rc;
+  MergeArgsHost a{};
+  a.src = dst->self_scratch->st;
+  a.mode = 0;
+  return run_merge(dst, a, s);
 }
 
 int gk_fold_packed(gk_set* dst, const void* const* bufs, int nbufs, void* stream) {

@@ -189,6 +189,33 @@ def run_merge_case(ref, st, cid, eps, shards):
     st.put_tables(pre + "/merged_final", [snap(acc)])
 
 
+def run_merge_plan_case(ref, st, cid, eps, shards, plan):
+    """sk[0].merge(sk[p]) for p in plan, in order; p == 0 merges the sketch
+    into itself (the reference accepts it: gk:111-154)."""
+    sks = []
+    for xs in shards:
+        sk = ref.GKArray(eps)
+        for x in xs:
+            sk.add(V(x))
+        sks.append(sk)
+    pre = "case%d" % cid
+    st.put(pre + "/shard_sizes", [len(s) for s in shards], np.int64)
+    st.put(pre + "/x", np.concatenate([np.asarray(s, dtype=np.float64) for s in shards]), np.float64)
+    st.put(pre + "/plan", plan, np.int64)
+    acc = sks[0]
+    steps, srcs = [], []
+    for p in plan:
+        acc.merge(sks[p])
+        steps.append(snap(acc))
+        srcs.append(snap(sks[p]))
+    st.put_tables(pre + "/merge_steps", steps)
+    st.put_tables(pre + "/others_after", srcs)
+    st.put(pre + "/merged_stats", stats(acc), np.float64)
+    st.put(pre + "/merged_pending", [float(p) for p in acc.incoming], np.float64)
+    st.put(pre + "/merged_q", [float(v) for v in acc.quantiles(QS)], np.float64)
+    st.put_tables(pre + "/merged_final", [snap(acc)])
+
+
 def main():
     ref = load_reference()
     st = Store()
@@ -312,6 +339,23 @@ def main():
             run_merge_case(ref, st, cid, eps, shards)
             st.index.append(dict(id=cid, kind="merge", eps=eps, dist="lognormal", k=k))
             cid += 1
+
+    # -- 7. merge plans: a.merge(a) (gk:111-154 with other IS self: the flush
+    #       of gk:137 empties self's own incoming, gk:149 doubles _n) and
+    #       repeated sources (a.merge(b); a.merge(b): b is flushed twice) --
+    #       appended last so that the cases above keep their ids and draws
+    rng7 = np.random.default_rng(20261018)
+    for eps in [0.1, 0.01]:
+        P = int(1.0 / eps) + 1
+        for L in [0, 1, 5, 3 * P, 3 * P + 5, 9 * P + 40]:
+            for dist in ["uniform", "zeros"]:
+                for plan in ([0], [0, 0], [1, 0], [1, 1], [0, 1, 0]):
+                    lens = [L] + ([int(rng7.integers(1, 4 * P))] if 1 in plan else [])
+                    shards = [gen_values(dist, int(n), rng7) for n in lens]
+                    run_merge_plan_case(ref, st, cid, eps, shards, plan)
+                    st.index.append(dict(id=cid, kind="merge_plan", eps=eps, dist=dist, L=int(L),
+                                         plan=list(plan)))
+                    cid += 1
 
     np.savez_compressed(os.path.join(HERE, "golden.npz"), **st.arrays)
     with open(os.path.join(HERE, "golden_index.json"), "w") as f:

@@ -96,6 +96,42 @@ def assert_same_quantiles(got, exp, what, unpinned):
     assert not bad, "%s: %d mismatches, first %r" % (what, len(bad), bad[:3])
 
 
+def check_golden_merge_plans(dev):
+    """The reference's merge plans (make_golden.py section 7): sk[0].merge(sk[p])
+    for p in the plan, p == 0 merging a sketch into ITSELF (gk:111-154) and
+    repeated sources.  The cases of one (eps, plan) run batched, one stream
+    each, through StreamSet.merge_from([self]) / merge_from([src]); every
+    step's destination and source tables, the final stats and quantiles are
+    compared with the reference's.  Returns the number of cases checked."""
+    groups = {}
+    for c in G.cases("merge_plan"):
+        groups.setdefault((c["eps"], tuple(c["plan"])), []).append(c)
+    checked = 0
+    for (eps, plan), cs in groups.items():
+        nsh = max(plan) + 1
+        sets = []
+        for j in range(nsh):
+            ss = _ss(len(cs), eps, dev)
+            ingest_np(ss, [G.shards(c["id"])[j] for c in cs])
+            sets.append(ss)
+        for k, p in enumerate(plan):
+            sets[0].merge_from([sets[p]])
+            for i, c in enumerate(cs):
+                assert G.same_table(sets[0].table(i), G.tables(c["id"], "merge_steps")[k]), (c, k)
+                assert G.same_table(sets[p].table(i), G.tables(c["id"], "others_after")[k]), (c, k)
+        st = {k: v.cpu().numpy() for k, v in sets[0].stats().items()}
+        q = sets[0].quantiles(G.index()["qs"]).cpu().numpy()
+        for i, c in enumerate(cs):
+            got = [st["n"][i], st["min"][i], st["max"][i], st["sum"][i], st["avg"][i]]
+            assert all(G.same_float(a, b) for a, b in zip(got, G.get(c["id"], "merged_stats"))), (c, got)
+            assert_same_quantiles(q[i], G.get(c["id"], "merged_q"), c,
+                                  golden_mask(G.tables(c["id"], "merge_steps")[-1], st["n"][i], eps,
+                                              G.index()["qs"]))
+            assert G.same_table(sets[0].table(i), G.tables(c["id"], "merged_final")[0]), c
+            checked += 1
+    return checked
+
+
 def gen(dist, L, rng):
     if dist == 0:
         return rng.random(L)

@@ -25,17 +25,23 @@ def free_port():
         return s.getsockname()[1]
 
 
-def run_bench(args, world, dump, env_extra=None):
+def run_bench(args, world, dump, env_extra=None, launcher="torchrun"):
+    """launcher "torchrun": the driver's form (torch.distributed.run ... bench.py
+    --gpus N); "self": plain `bench.py --gpus N`, which starts the N ranks."""
     env = dict(os.environ, OMP_NUM_THREADS="4", **(env_extra or {}))
-    if world == 1:
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    if world == 1 or launcher == "self":
         cmd = [sys.executable, BENCH]
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % world,
                "--master-addr=127.0.0.1", "--master-port=%d" % free_port(), BENCH]
-    cmd += args + ["--steps", "1", "--warmup", "0", "--no-cpu", "--dump", dump]
+    cmd += args + ["--gpus", str(world), "--steps", "1", "--warmup", "0", "--no-cpu", "--dump", dump]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
-    return json.loads(r.stdout.strip().splitlines()[-1])
+    lines = [ln for ln in r.stdout.strip().splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]  # rank 0's line only
+    return json.loads(lines[0])
 
 
 def gather(dump, world, S):
@@ -48,10 +54,10 @@ def gather(dump, world, S):
     return q, parts
 
 
-def check_split(tmp_path, args, S, world, device_args, env_extra=None, min_ranks_len_ratio=None):
+def check_split(tmp_path, args, S, world, device_args, env_extra=None, launcher="torchrun"):
     one = run_bench(args + device_args, 1, str(tmp_path / "one"), env_extra)
-    assert one["scaling"] == "weak" and one["config"]["split"] == "weak"
-    line = run_bench(args + device_args, world, str(tmp_path / "split"), env_extra)
+    assert one["scaling"] == "weak" and one["config"]["split"] == "weak" and one["n_gpus"] == 1
+    line = run_bench(args + device_args, world, str(tmp_path / "split"), env_extra, launcher)
     assert line["scaling"] == "strong" and line["config"]["split"] == "strong" and line["n_gpus"] == world
     assert "weak" in line and line["weak"]["scaling"] == "weak"
     q1 = np.load(str(tmp_path / "one") + ".rank0.npz")["q"]
@@ -64,6 +70,22 @@ def check_split(tmp_path, args, S, world, device_args, env_extra=None, min_ranks
 def test_strong_split_cfg3_cpu(tmp_path, world):
     check_split(tmp_path, ["--workload", "cfg3", "--streams", "1500", "--values", "1000"], 1500, world,
                 ["--device", "cpu"])
+
+
+def test_gpus_flag_starts_the_ranks_cpu(tmp_path):
+    """`bench.py --gpus 3` with no launcher around it runs 3 ranks (VERDICT r04
+    item 2: --gpus used to be ignored), strong split bit-identical to 1 rank."""
+    check_split(tmp_path, ["--workload", "cfg3", "--streams", "900", "--values", "500"], 900, 3,
+                ["--device", "cpu"], launcher="self")
+
+
+def test_gpus_flag_must_match_the_world(tmp_path):
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", "--master-port=%d" % free_port(), BENCH, "--gpus", "3", "--device", "cpu",
+           "--streams", "100", "--values", "100", "--steps", "1", "--warmup", "0", "--no-cpu"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode != 0 and "launcher started 2 rank(s)" in r.stderr
 
 
 def test_strong_split_cfg5_balanced_cpu(tmp_path):
@@ -83,6 +105,22 @@ def test_strong_split_cfg3_rehearsal_on_device(tmp_path):
         pytest.skip("no GPU")
     check_split(tmp_path, ["--workload", "cfg3", "--streams", "20000", "--values", "1000"], 20000, 2, [],
                 env_extra={"GK_BENCH_REHEARSE": "1"})
+
+
+@pytest.mark.gpu
+def test_gpus_flag_on_device(tmp_path):
+    """`GK_BENCH_REHEARSE=1 bench.py --gpus 2` runs two ranks on one card and
+    prints n_gpus 2; `bench.py --gpus K` beyond the node's GPUs fails loudly."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    check_split(tmp_path, ["--workload", "cfg3", "--streams", "20000", "--values", "1000"], 20000, 2, [],
+                env_extra={"GK_BENCH_REHEARSE": "1"}, launcher="self")
+    n = torch.cuda.device_count()
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "GK_BENCH_REHEARSE")}
+    r = subprocess.run([sys.executable, BENCH, "--gpus", str(n + 1), "--steps", "1", "--warmup", "0", "--no-cpu"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode != 0 and "GPU(s)" in r.stderr, r.stderr[-2000:]
 
 
 @pytest.mark.gpu

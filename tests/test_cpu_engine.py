@@ -10,7 +10,8 @@ import torch
 
 import golden_io as G
 from gk_oracle_c import OracleSet
-from parity_util import (_ss, assert_same_quantiles, assert_same_state, assert_same_tables, csr, gen, ingest_np,
+from parity_util import (_ss, assert_same_quantiles, assert_same_state, assert_same_tables, check_golden_merge_plans, csr,
+                         gen, ingest_np,
                          golden_mask, small_of)
 
 CPU = "cpu"
@@ -93,6 +94,27 @@ def test_golden_merges_and_query_mid_cpu():
             assert_same_quantiles(ss.quantiles([0.1, 0.5, 0.9]).numpy()[0], G.get(cid, "mid_q")[k], c,
                                   golden_mask(G.tables(cid, "mid_tables")[k], p, eps, [0.1, 0.5, 0.9]))
             prev = p
+
+
+def test_golden_merge_plans_cpu():
+    """a.merge(a) and repeated sources (gk:111-154) against the reference."""
+    assert check_golden_merge_plans(CPU) == len(G.cases("merge_plan")) > 100
+
+
+def test_dropin_self_merge_cpu():
+    from gkarray_amd import GKArray
+    from gk_oracle import OracleGK
+    rng = np.random.default_rng(7)
+    xs = rng.lognormal(0, 1, 1234)
+    sk, o = GKArray(0.01, device=CPU), OracleGK(0.01)
+    for x in xs:
+        sk.add(x)
+    o.add_many(xs)
+    sk.merge(sk)
+    o.merge(o)
+    assert sk._n == o.n == 2468
+    assert [(e.val, e.g, e.delta) for e in sk.entries] == o.table()
+    assert sk.quantiles([.5, .9]) == o.quantiles([.5, .9])
 
 
 @pytest.mark.parametrize("eps", [0.2, 0.05, 0.03, 0.015, 0.01, 0.001, 0.0005, 0.0002])

@@ -20,8 +20,8 @@ import torch
 
 import golden_io as G
 from gk_oracle_c import OracleSet
-from parity_util import (_ss, assert_same_quantiles, assert_same_state, assert_same_tables, csr, gen,
-                         ingest_np, golden_mask, small_of, tables_np)
+from parity_util import (_ss, assert_same_quantiles, assert_same_state, assert_same_tables,
+                         check_golden_merge_plans, csr, gen, ingest_np, golden_mask, small_of, tables_np)
 
 pytestmark = pytest.mark.gpu
 
@@ -103,6 +103,44 @@ def test_golden_merges(gpu_device):
         assert all(G.same_float(a, b) for a, b in zip(got, G.get(cid, "merged_stats"))), c
         assert_same_quantiles(acc.quantiles(G.index()["qs"]).cpu().numpy()[0], G.get(cid, "merged_q"), c,
                               golden_mask(steps[-1], st["n"][0], eps, G.index()["qs"]))
+
+
+def test_golden_merge_plans(gpu_device):
+    """a.merge(a) and repeated sources (gk:111-154) against the reference: the
+    self-merge runs from a snapshot of the flushed set (gk_capi.cpp
+    merge_self), bit-exact to every step of the reference's plan."""
+    assert check_golden_merge_plans(gpu_device) == len(G.cases("merge_plan")) > 100
+
+
+def test_dropin_self_merge(gpu_device):
+    from gkarray_amd import GKArray
+    from gk_oracle import OracleGK
+    xs = np.random.default_rng(7).lognormal(0, 1, 1234)
+    sk, o = GKArray(0.01), OracleGK(0.01)
+    for x in xs:
+        sk.add(x)
+    o.add_many(xs)
+    sk.merge(sk)
+    o.merge(o)
+    assert sk._n == o.n == 2468
+    assert [(e.val, e.g, e.delta) for e in sk.entries] == o.table()
+    assert sk.quantiles([.5, .9]) == o.quantiles([.5, .9])
+    # StreamSet: the set itself inside a longer source list, at scale
+    rng = np.random.default_rng(8)
+    S, eps = 3000, 0.01
+    seqs = [gen(int(d), int(L), rng) for d, L in zip(rng.integers(0, 8, S), rng.integers(0, 3000, S))]
+    other = [gen(1, int(L), rng) for L in rng.integers(0, 3000, S)]
+    a, b = _ss(S, eps, gpu_device), _ss(S, eps, gpu_device)
+    oa, ob = OracleSet(S, eps), OracleSet(S, eps)
+    ingest_np(a, seqs)
+    ingest_np(b, other)
+    oa.ingest(*csr(seqs))
+    ob.ingest(*csr(other))
+    a.merge_from([b, a, b, a])
+    for src in (ob, oa, ob, oa):
+        oa.merge(src)
+    assert_same_state(a, oa, "self-merge fold")
+    assert_same_state(b, ob, "repeated source")
 
 
 def test_eps_mismatch(gpu_device):

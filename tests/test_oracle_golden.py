@@ -175,6 +175,55 @@ def test_oracles_merge(case):
                                                                    n_acc, eps, G.index()["qs"]))
 
 
+def check_merge_plan(case, build, table, stats_of, quantiles):
+    """sk[0].merge(sk[p]) for p in the case's plan (p == 0: the sketch merged
+    into itself, gk:111-154), every step's destination and source table, the
+    final stats and quantiles against the reference's (make_golden.py 7)."""
+    cid, eps = case["id"], case["eps"]
+    sk = [build(xs) for xs in G.shards(cid)]
+    steps, srcs = G.tables(cid, "merge_steps"), G.tables(cid, "others_after")
+    for k, p in enumerate(int(p) for p in G.get(cid, "plan")):
+        sk[0].merge(sk[p])
+        assert G.same_table(table(sk[0]), steps[k]), (case, k)
+        assert G.same_table(table(sk[p]), srcs[k]), (case, k)
+    got = stats_of(sk[0])
+    assert all(G.same_float(a, b) for a, b in zip(got, G.get(cid, "merged_stats"))), (case, got)
+    assert_qs(quantiles(sk[0]), G.get(cid, "merged_q"), case,
+              G.unpinned_mask(steps[-1], got[0], eps, G.index()["qs"]))
+    assert G.same_table(table(sk[0]), G.tables(cid, "merged_final")[0]), case
+
+
+MERGE_PLANS = G.cases("merge_plan")
+
+
+@pytest.mark.parametrize("case", MERGE_PLANS, ids=lambda c: "c%d-e%s-L%d-%s" % (c["id"], c["eps"], c["L"], c["plan"]))
+def test_oracles_merge_plan(case):
+    eps = case["eps"]
+
+    def py(xs):
+        o = OracleGK(eps)
+        o.add_many(xs)
+        return o
+
+    def c(xs):
+        o = OracleSet(1, eps)
+        o.ingest(xs, [0, len(xs)])
+        return o
+
+    check_merge_plan(case, py, lambda o: o.table(), lambda o: [o.n, o.min, o.max, o.sum, o.avg],
+                     lambda o: o.quantiles(G.index()["qs"]))
+    check_merge_plan(case, c, lambda o: o.table(0),
+                     lambda o: [o.stats()[k][0] for k in ("n", "min", "max", "sum", "avg")],
+                     lambda o: o.quantiles(G.index()["qs"])[0])
+
+
+def test_merge_plans_cover_self_merge():
+    plans = [c["plan"] for c in MERGE_PLANS]
+    assert [0] in plans and [0, 0] in plans and [1, 0] in plans and [1, 1] in plans
+    assert {c["L"] for c in MERGE_PLANS} >= {0, 1, 5}  # empty, small-n
+    assert {c["eps"] for c in MERGE_PLANS} == {0.1, 0.01}
+
+
 def test_eps_mismatch_raises():
     assert any(c["kind"] == "eps_mismatch" and c["raised"] for c in G.index()["cases"])
     a, b = OracleGK(0.01), OracleGK(0.02)
