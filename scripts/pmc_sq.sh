@@ -1,6 +1,6 @@
 # SQ counter passes (one rocprofv3 --pmc run each, no tracing domains) on the
 # default bench step, k_ingest_small only (KRX: another kernel regex, e.g.
-# k_ingest_half with GK_HALF=1 in the environment).  Usage: pmc_sq.sh TAG
+# k_ingest_wg with a cfg5 bench command).  Usage: pmc_sq.sh TAG
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 TAG=${1:-sq}

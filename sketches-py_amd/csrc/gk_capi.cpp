@@ -861,9 +861,12 @@ int run_ingest(gk_set* h, const double* x, const int64_t* offs, int force, hipSt
                                 ovf_list(h, 0), wwork, h->ps, h->aux2));
     HIP_TRY(hipEventRecord(h->ev_wg, h->aux2));
   }
-  HIP_TRY(launch_class(h, 0, x, offs, nullptr, nullptr, 0, force, q, stream, prio && x != nullptr, wg));
-  // (its overflow entries feed the promotion rounds below)
+  const hipError_t lc = launch_class(h, 0, x, offs, nullptr, nullptr, 0, force, q, stream, prio && x != nullptr, wg);
+  // (its overflow entries feed the promotion rounds below).  k_ingest_wg is
+  // joined on every path once launched: the next call's begin_call zeroes the
+  // counter block it adds to
   if (wg) HIP_TRY(hipStreamWaitEvent(stream, h->ev_wg, 0));
+  HIP_TRY(lc);
   // (with k_ingest_wg beside it, the timed span is both: the call's batch ingest)
   hipEvent_t t1 = timed ? timing_event(h->tev_flush, h->n_flush) : nullptr;
   if (t1) HIP_TRY(hipEventRecord(t1, stream));
@@ -1093,6 +1096,7 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
   okm &= hipHostMalloc(&h->h_hc_flag, sizeof(unsigned long long), hipHostMallocCoherent | hipHostMallocMapped) ==
          hipSuccess;
   okm &= hipMalloc(&h->d_hc_fail, sizeof(int32_t)) == hipSuccess;
+  okm &= h->d_hc_fail && hipMemset(h->d_hc_fail, 0, sizeof(int32_t)) == hipSuccess;
   if (h->h_hc_flag) *h->h_hc_flag = 0;
   if (const char* e = getenv("GK_HC_FAIL")) h->hc_fail_inject = atoi(e) != 0;
   okm &= hipEventCreateWithFlags(&h->ev_hc, hipEventDisableTiming) == hipSuccess;
@@ -1743,8 +1747,16 @@ int gk_capacity(const gk_set* h, int cls) {
 int64_t gk_host_chains_taken(gk_set* h) {
   if (!h) return -1;
   hc_drain(h);
+  // the device's verdict on the last host-walked call: k_hc_wait sets the
+  // fail word when the worker reported a failure or its flag came too late
+  // (the chains were then walked on the device: k_hc_fallback), even if the
+  // worker finished OK afterwards
+  int32_t dev_fail = 0;
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(&dev_fail, h->d_hc_fail, sizeof(dev_fail), hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
   std::lock_guard<std::mutex> lk(h->hc_mu);
-  return h->hc_last_rc == GK_OK ? h->hc_last_taken : 0;
+  return (h->hc_last_rc == GK_OK && dev_fail == 0) ? h->hc_last_taken : 0;
 }
 
 int64_t gk_num_promoted(const gk_set* h) {

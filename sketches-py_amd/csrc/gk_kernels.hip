@@ -1921,9 +1921,6 @@ __device__ __forceinline__ void wg_sort(WgLDS& L, double (&xv)[GK_WG_VPT], int c
 #ifndef GK_WG_RK_UNROLL
 #define GK_WG_RK_UNROLL 4
 #endif
-#ifndef GK_WG_SEARCH8
-#define GK_WG_SEARCH8 0  // 8-ary rounds: measured no faster (r04n: search 2.31e8 vs 2.23e8 cycles, cfg5 49.7 vs 49.1-49.4 ms)
-#endif
 __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG_VPT], const int cnt,
                         const int T, const int t, bool sorted) {
   const int lane = t & 63, w = t >> 6;
@@ -1968,40 +1965,6 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
   for (int pass = 0;; ++pass) {
 #pragma unroll
     for (int r = 0; r < GK_WG_VPT; ++r) xg[r] = 0;
-#if GK_WG_SEARCH8
-    // 8-ary rounds (7 probes issued together: 4 dependent LDS round trips
-    // for a 1024-slot table instead of 10), then 4- / 2-ary for the rest
-    {
-      const int P2 = gk_pow2_above(E);
-      int bits = 31 - __builtin_clz(P2);  // log2(P2)
-      int step = P2;
-      while (bits >= 3) {
-        step >>= 3;
-        bits -= 3;
-        double tt[GK_WG_VPT][7];
-#pragma unroll
-        for (int r = 0; r < GK_WG_VPT; ++r)
-#pragma unroll
-          for (int k = 0; k < 7; ++k) tt[r][k] = tv[xg[r] + (k + 1) * step - 1];
-#pragma unroll
-        for (int r = 0; r < GK_WG_VPT; ++r) {
-          int c = 0;
-#pragma unroll
-          for (int k = 0; k < 7; ++k) c += (tt[r][k] <= xv[r]) ? 1 : 0;
-          xg[r] += c * step;
-        }
-      }
-      while (bits > 0) {
-        step >>= 1;
-        --bits;
-        double tt[GK_WG_VPT];
-#pragma unroll
-        for (int r = 0; r < GK_WG_VPT; ++r) tt[r] = tv[xg[r] + step - 1];
-#pragma unroll
-        for (int r = 0; r < GK_WG_VPT; ++r) xg[r] += (tt[r] <= xv[r]) ? step : 0;
-      }
-    }
-#else
     for (int step = gk_pow2_above(E) >> 1; step > 0; step >>= 1) {
       double tt[GK_WG_VPT];
 #pragma unroll
@@ -2009,7 +1972,6 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
 #pragma unroll
       for (int r = 0; r < GK_WG_VPT; ++r) xg[r] += (tt[r] <= xv[r]) ? step : 0;
     }
-#endif
 #pragma unroll
     for (int r = 0; r < GK_WG_VPT; ++r) xg[r] = min(xg[r], E);
     if (pass > 0) {  // (the re-search of a sorted batch: counts start over)
@@ -2335,7 +2297,8 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
 #pragma unroll
         for (int r = 0; r < GK_WG_VPT; ++r) xv[r] = xn[r];
         cur_sorted = next_sorted;
-      } else if (sb && ps_ok) {
+      } else if (sb && ps_ok && (flushed || !ps_done)) {
+        // (beside the presort, batch 0 is never sorted: k_presort_reg)
         cur_sorted = true;
 #pragma unroll
         for (int r = 0; r < GK_WG_VPT; ++r) {
@@ -2817,32 +2780,15 @@ __global__ __launch_bounds__(64) void k_ingest_big(GKState st, const double* __r
 //    prefix(g) + d - 1, one ballot + popcount per entry slot and quantile.
 // ===========================================================================
 #define SMALL_CAP GK_SMALL_CAP
-// Round-4 variants of the small class, measured on MI355X and left OFF in
-// the product build (profiles/r04f_ab.txt, cfg3 k_ingest_small launch vs
-// 5.98-5.99 ms): GD16 6.06-6.09 ms (+1.4%: fewer LDS cycles, more VALU and
-// a longer chain), TPRED 6.06 ms (+1.2%), ZSEL 5.92-6.00 ms (within noise).
-// entry (g, d) of the LDS table packed in 32 bits (1) or as two int32 (0)
-#ifndef GK_GD16
-#define GK_GD16 0
-#endif
-#ifndef GK_TPRED
-#define GK_TPRED 0  // T and its divider made one flush ahead
-#endif
-#ifndef GK_ZSEL
-#define GK_ZSEL 0  // zero only the count words a flush set
-#endif
+// Round-4 variants of the small class were measured on MI355X and removed
+// ((g, d) packed in 32 bits, T one flush ahead, selective
+// count zeroing, masked in-gap rank reads, every batch register-sorted).
 #ifndef GK_SMALL_WAVES
 #define GK_SMALL_WAVES 6  // min waves per SIMD asked of the register allocator
 #endif
 // largest gap handled by the in-gap rank loop; larger gaps rank by counting
 #ifndef GK_SMALL_RANK_MAX
 #define GK_SMALL_RANK_MAX 16
-#endif
-// in-gap rank reads: 0 = every lane reads past its members (into the next
-// gaps and a +inf pad), 1 = exec-masked to the lane's own members, 2 = lanes
-// past their members read one +inf slot
-#ifndef GK_RK_MASK
-#define GK_RK_MASK 0
 #endif
 // Compiler-only barrier between two LDS accesses: keeps adjacent 8-byte
 // reads as separate ds_read_b64 (2 LDS cycles each, banks over 64 dwords)
@@ -2908,15 +2854,7 @@ struct SmallLDS {
   // as ds_read2_b64 immediates
   alignas(16) double mv[64 * VPL + 64 + 2];  // values grouped by gap, +inf after the last; [last] trash
   alignas(16) double tv[SMALL_TVN];        // entry values at pidx(i); +inf from E up to E+63 (<= 127)
-#if GK_GD16
-  // entry (g, d) at i packed in one word (g low 16 bits, d high 16 bits,
-  // both unsigned: the stream's load checks g, d >= 0 and g + d <= 65535,
-  // which every flush of the add path keeps while T <= 65535, DESIGN.md
-  // §5); [j0+2] read as successor; [129] trash
-  alignas(16) uint32_t tgd[SMALL_CAP + 4];
-#else
   alignas(16) int2 tgd[SMALL_CAP + 2];     // entry (g, d) at i; [j0+2] read as successor; [129] trash
-#endif
   union {
     // per gap (padded index): first the member count (.x, the count atomics),
     // then the record (m<<24 | k<<16 | member base<<8 | out base, G+d-1)
@@ -2926,9 +2864,6 @@ struct SmallLDS {
     // and the records are reset (zeroed) after the pass.
     int32_t mi[64 * VPL + 2];
   };
-#ifdef GK_LDS_PAD
-  unsigned char pad[GK_LDS_PAD];  // occupancy experiments only
-#endif
 #ifdef GK_PROF
   unsigned long long prof[GK_PROF_NSEC];
   uint32_t prof_t;
@@ -2993,15 +2928,11 @@ __device__ __forceinline__ int gd_d(uint32_t w) { return (int)(w >> 16); }
 template <int VPL, int DUPG = -1>
 __device__ __forceinline__ void small_put(SmallLDS<VPL>& L, int pos, double v, int g, int d) {
   L.tv[pidx(pos)] = v;
-#if GK_GD16
-  L.tgd[pos] = gd_pack(g, d);
-#else
   L.tgd[pos] = make_int2(g, d);
   if constexpr (DUPG >= 0 && GK_DUPG(DUPG)) {
     dup_st(&L.tv[pidx(pos)], v);
     dup_st(&L.tgd[pos], make_int2(g, d));
   }
-#endif
 }
 
 // gi[gap].x = m << 24 | k << 16 | member base << 8 | out base (m, k <= 128)
@@ -3220,7 +3151,7 @@ __device__ void presort_reg_range(const GKState& st, const double* __restrict__ 
                                   const int32_t* __restrict__ list, const int cnt,
                                   const int64_t* __restrict__ list_n, const int64_t* __restrict__ list_ws,
                                   const int64_t* __restrict__ list_b0, double* __restrict__ ws, uint8_t* zs,
-                                  const int lane);
+                                  const int lane, const bool skip0);
 
 __global__ __launch_bounds__(64) void k_presort_reg(GKState st, const double* __restrict__ x,
                                                     const int64_t* __restrict__ offs,
@@ -3233,7 +3164,12 @@ __global__ __launch_bounds__(64) void k_presort_reg(GKState st, const double* __
   __shared__ uint8_t zs[64 * GK_PS_R];
   const int cnt = *count;
   const int lane = threadIdx.x;
-  if (cnt > 0) presort_reg_range(st, x, offs, list, cnt, list_n, list_ws, list_b0, ws, zs, lane);
+  // Beside k_ingest_wg (done != null) a stream's batch 0 is not sorted: it
+  // holds the stream's pre-call pending values, and k_ingest_wg may finish
+  // that stream -- rewriting st.pend and its pbuf -- before this launch reaches
+  // it; k_ingest_wg ranks every call's first batch unsorted then.
+  // Batches b >= 1 are P values of the call's input: read-only here and there.
+  if (cnt > 0) presort_reg_range(st, x, offs, list, cnt, list_n, list_ws, list_b0, ws, zs, lane, done != nullptr);
   // (k_ingest_wg, running beside this launch, takes presorted batches once
   // every wave has counted itself here: release of this wave's stores)
   if (done) {
@@ -3246,7 +3182,7 @@ __device__ void presort_reg_range(const GKState& st, const double* __restrict__ 
                                   const int32_t* __restrict__ list, const int cnt,
                                   const int64_t* __restrict__ list_n, const int64_t* __restrict__ list_ws,
                                   const int64_t* __restrict__ list_b0, double* __restrict__ ws, uint8_t* zs,
-                                  const int lane) {
+                                  const int lane, const bool skip0) {
   const int64_t total = list_b0[cnt];
   const int P = st.P;
   // a contiguous range of global batches per wave (as k_presort)
@@ -3277,11 +3213,14 @@ __device__ void presort_reg_range(const GKState& st, const double* __restrict__ 
       b0 = list_b0[i];
       s = list[i];
       xo = offs[s];
-      p = st.pend[s];
       need = P - (list_n[i] % P);
     }
     if (wso < 0) continue;
     const int64_t b = gb - b0;
+    if (b == 0) {
+      if (skip0) continue;  // wave-uniform
+      p = st.pend[s];  // the pre-call pending values: nothing writes them during this launch
+    }
     const double* pb = st.pbuf + s * (int64_t)st.pmax;
     const int m = b == 0 ? p + (int)need : P;
     const int64_t xb = b == 0 ? xo : xo + need + (b - 1) * P;
@@ -3338,27 +3277,12 @@ __device__ void presort_reg_range(const GKState& st, const double* __restrict__ 
 // One flush of the small class; K entries per lane (E <= 64*K - 1).  Returns
 // the new table size, or -1 if it would exceed SMALL_CAP-1 (the table is then
 // untouched... except for the counts, which the caller discards).
-#ifndef GK_SORTALL
-#define GK_SORTALL 0
-#endif
 template <int VPL, int K, typename AfterSearch>
 __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const double (&xv_in)[VPL], const int cnt,
                                            const int T, const CsDiv cd, const int lane, AfterSearch&& after_search) {
   static_assert(K == 2, "the 128-entry class holds 2 entries per lane");
-#if GK_SORTALL
-  // (experiment, VERDICT r03 1(d): every flush's batch sorted in registers
-  // first, ranks = position - gap member base, no member stores / rank loop)
-  double xv[VPL];
-#pragma unroll
-  for (int r = 0; r < VPL; ++r) xv[r] = xv_in[r];
-  bool sorted_batch = false;
-#else
   const double (&xv)[VPL] = xv_in;
-  constexpr bool sorted_batch = false;
-#endif
-  // cd = make_csdiv(T): the chunk-size divider, made by the caller (for an
-  // automatic flush one flush ahead, so that its magic-number scalar load is
-  // not waited for on the flush's critical path)
+  // cd = make_csdiv(T): the chunk-size divider, made by the caller
   if constexpr (VPL == 2) {
     // ---- empty table (every stream's first flush): all values are tail
     //      (gk:85-92), so the flush is a sort and a cut into chunks of
@@ -3396,27 +3320,6 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
       }
     }
   }
-#if GK_SORTALL
-  if constexpr (VPL == 2) {
-    bool pz = false, nz = false;
-#pragma unroll
-    for (int r = 0; r < VPL; ++r) {
-      const bool z = (lane + 64 * r < cnt) && xv[r] == 0.0;
-      pz |= z && !signbit(xv[r]);
-      nz |= z && signbit(xv[r]);
-    }
-    if (!(__builtin_amdgcn_ballot_w64(pz) != 0 && __builtin_amdgcn_ballot_w64(nz) != 0)) {
-      double a[2];
-#pragma unroll
-      for (int r = 0; r < 2; ++r)
-        a[r] = (lane + 64 * r < cnt) ? xv[r] : __longlong_as_double(0x7ff0000000000000LL);
-      sort128_2(a, lane);
-      xv[0] = a[0];
-      xv[1] = a[1];
-      sorted_batch = true;
-    }
-  }
-#endif
   // ---- gap = #entries <= x (gk:93): 7 levels over the padded table ---------
   // (slots E .. E+63 hold +inf, small_pad).  xb: byte offset of the padded
   // slot of the gap's entry; x = +inf may step into the padding: clamped to
@@ -3460,21 +3363,11 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
   int eg[K + 1], ed[K + 1], em[K];
   {
     int2 gd[K + 1];
-#if GK_GD16
-    {
-      const uint2 a = *(const uint2*)&L.tgd[j0];
-      const uint32_t a2 = L.tgd[j0 + 2];
-      gd[0] = make_int2(gd_g(a.x), gd_d(a.x));
-      gd[1] = make_int2(gd_g(a.y), gd_d(a.y));
-      gd[2] = make_int2(gd_g(a2), gd_d(a2));
-    }
-#else
     const int4 a = *(const int4*)&L.tgd[j0];
     gd[0] = make_int2(a.x, a.y);
     gd[1] = make_int2(a.z, a.w);
     gd[2] = L.tgd[j0 + 2];
-#endif
-    if constexpr (!GK_GD16 && GK_DUPG(4)) {
+    if constexpr (GK_DUPG(4)) {
       dup_ld((const int4*)&L.tgd[j0]);
       dup_ld(&L.tgd[j0 + 2]);
       dup_ld(&L.tv[pj0]);
@@ -3622,16 +3515,7 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
   GK_MARK(L, 4);
 
   // ---- stable order inside each gap (gk:72), then emit --------------------
-  if (sorted_batch) {
-    // (GK_SORTALL) sorted: a gap's members are contiguous, rank = position -
-    // the gap's member base
-#pragma unroll
-    for (int r = 0; r < VPL; ++r) {
-      const int2 gv = *(const int2*)((const char*)L.gi + xb[r]);
-      small_emit(L, xb[r] < pE8, cd, xv[r], gv, lane + 64 * r - gi_mb(gv.x), lane + 64 * r < cnt);
-    }
-    GK_MARK(L, 5);
-  } else if (!use_sort) {
+  if (!use_sort) {
     // Members of a gap are stored in slot order (the atomic slot xs).  A
     // value's rank in its gap counts the members below it.  Fast pass:
     // strict counts over every member (self included: never below itself);
@@ -3648,8 +3532,6 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
     int omax = 0;  // this lane's largest member count; the loop runs while any lane needs it
     int dsum = 0;  // sum over this lane's values of (members - 1)
     constexpr int MV_TRASH = 64 * VPL + 64 + 1;
-    constexpr int MV_INF = 64 * VPL + 64;  // +inf for the whole launch (GK_RK_MASK 2)
-    (void)MV_INF;
 #pragma unroll
     for (int r = 0; r < VPL; ++r) {
       const bool v = lane + 64 * r < cnt;
@@ -3660,19 +3542,12 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
       dsum += v ? m - 1 : 0;
       mm[r] = m >= 2 ? m : 0;  // a lone member has rank 0
       me[r] = (int)xs[r];
-#if GK_RK_MASK
-      // only members of gaps with m >= 2 are ever read
-      L.mv[(v && m >= 2) ? gb[r] + me[r] : MV_TRASH] = xv[r];
-#else
       L.mv[v ? gb[r] + me[r] : MV_TRASH] = xv[r];
-#endif
       if constexpr (GK_DUPG(6)) dup_st(&L.mv[v ? gb[r] + me[r] : MV_TRASH], xv[r]);
       omax = max(omax, mm[r]);
     }
-#if !GK_RK_MASK
     L.mv[totm + lane] = __longlong_as_double(0x7ff0000000000000LL);  // (>= GK_SMALL_RANK_MAX slots)
     if constexpr (GK_DUPG(6)) dup_st(&L.mv[totm + lane], __longlong_as_double(0x7ff0000000000000LL));
-#endif
     wsync<false>();
     int rk[VPL];
 #pragma unroll
@@ -3684,29 +3559,6 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
       // two ds_read_b64 -- 2 LDS cycles each over 64 banks -- instead of the
       // ds_read2_b64 the compiler would merge them into: 8 cycles, 32 banks)
       double y[VPL][2];
-#if GK_RK_MASK == 1
-      // exec-masked: a lane reads only while it has members left, so the
-      // reads of one instruction touch fewer distinct addresses (banks)
-#pragma unroll
-      for (int r = 0; r < VPL; ++r) {
-        y[r][0] = y[r][1] = __longlong_as_double(0x7ff0000000000000LL);
-        if (u0 < mm[r]) {
-          y[r][0] = L.mv[gb[r] + u0];
-          gk_lds_order();
-          const double t = L.mv[gb[r] + u0 + 1];  // one past the members: masked below
-          y[r][1] = (u0 + 1 < mm[r]) ? t : __longlong_as_double(0x7ff0000000000000LL);
-        }
-      }
-#elif GK_RK_MASK == 2
-      // lanes without members left read one fixed +inf slot (a broadcast)
-#pragma unroll
-      for (int r = 0; r < VPL; ++r) {
-        y[r][0] = L.mv[(u0 < mm[r]) ? gb[r] + u0 : MV_INF];
-        gk_lds_order();
-        y[r][1] = L.mv[(u0 + 1 < mm[r]) ? gb[r] + u0 + 1 : MV_INF];
-        gk_lds_order();
-      }
-#else
 #pragma unroll
       for (int r = 0; r < VPL; ++r) {
         y[r][0] = L.mv[gb[r] + u0];
@@ -3718,7 +3570,6 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
           dup_ld(&L.mv[gb[r] + u0 + 1]);
         }
       }
-#endif
 #pragma unroll
       for (int r = 0; r < VPL; ++r) rk[r] += ((y[r][0] < xv[r]) ? 1 : 0) + ((y[r][1] < xv[r]) ? 1 : 0);
     }
@@ -3806,18 +3657,7 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
     GK_MARK(L, 6);
   }
   small_pad(L.tv, newE, lane);
-#if GK_ZSEL
-  // zero exactly the count words this flush can have set: every gap's
-  // count and record live at its padded index, and the lanes' pairs
-  // (pj0, pj0+1) cover every padded index but 32/65/98, which never hold a
-  // gap (the tail pE included); the exact rank pass's member indices (mi)
-  // only reach those words' .y halves and index 32.  One ds_write2_b32 per
-  // lane instead of 1 088 bytes of zeros.
-  L.gi[pj0].x = 0;
-  L.gi[pj0 + 1].x = 0;
-#else
   small_zero_counts(L.gi, lane);
-#endif
   if constexpr (GK_DUPG(12)) {
     dup_st(&L.tv[pidx(min(newE + lane, SMALL_CAP - 1))], __longlong_as_double(0x7ff0000000000000LL));
     small_zero_counts(L.gi, lane);
@@ -3849,12 +3689,7 @@ __device__ __forceinline__ int small_rank_count(SmallLDS<VPL>& L, int E, int64_t
   const int j0 = 2 * lane;
   I run[2];
   {
-#if GK_GD16
-    const uint2 w = *(const uint2*)&L.tgd[j0];
-    const int4 gd = make_int4(gd_g(w.x), gd_d(w.x), gd_g(w.y), gd_d(w.y));
-#else
     const int4 gd = *(const int4*)&L.tgd[j0];
-#endif
     const int g0 = (j0 < E) ? gd.x : 0, g1 = (j0 + 1 < E) ? gd.z : 0;
     const I lsum = (I)g0 + (I)g1;
     I bex;
@@ -4098,9 +3933,6 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
   const int64_t pbeg = count * part / nparts, pend = count * (part + 1) / nparts;
   // the query's q values, the same for every stream: lane l holds q l
   const double qpre = (qs && lane < nq) ? qs[lane] : 0.0;
-#if GK_RK_MASK == 2
-  if (lane == 0) L.mv[64 * VPL + 64] = __longlong_as_double(0x7ff0000000000000LL);
-#endif
   int64_t cur = 0, cend = 0;
   auto grab = [&]() -> int64_t {
     if (cur >= cend) {
@@ -4146,26 +3978,12 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
 #pragma unroll
       for (int r = 0; r < SMALL_CAP / 64; ++r)
         rc[r] = (lane + 64 * r < E) ? t4[lane + 64 * r] : make_int4(0, 0, 0, 0);
-#if GK_GD16
-      // packed (g, d): every entry needs g, d >= 0 and g + d <= 65535, and
-      // the call's largest T must stay <= 65535 (then every flush keeps
-      // g + d <= 65535: DESIGN.md §5); else the stream takes the next class
-      bool bad = (double)(n + (Lx > 0 ? Lx : 0) - 1) * st.two_eps >= 65535.0;
-#pragma unroll
-      for (int r = 0; r < SMALL_CAP / 64; ++r)
-        bad |= (lane + 64 * r < E) && ((rc[r].z | rc[r].w) < 0 || rc[r].z + rc[r].w > 65535);
-      ok = __builtin_amdgcn_ballot_w64(bad) == 0;
-#endif
 #pragma unroll
       for (int r = 0; r < SMALL_CAP / 64; ++r) {
         const int j = lane + 64 * r;
         if (j < E) {
           L.tv[pidx(j)] = __hiloint2double(rc[r].y, rc[r].x);
-#if GK_GD16
-          L.tgd[j] = gd_pack(rc[r].z, rc[r].w);
-#else
           L.tgd[j] = make_int2(rc[r].z, rc[r].w);
-#endif
         }
       }
       small_pad(L.tv, E, lane);
@@ -4183,8 +4001,6 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
     // a multiply and a truncation (n >= 1 at every flush, and gk_count_ok
     // above bounds T by GK_T_CLAMP for the whole call: no clamps)
     double nm1 = (double)(n - 1);
-    int Tpred = -1;  // T and divider of the next automatic flush (made one flush ahead)
-    CsDiv cdpred = {1, 1u << 23};
     double xv[VPL];
 #pragma unroll
     for (int r = 0; r < VPL; ++r) xv[r] = 0.0;
@@ -4214,19 +4030,8 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
       };
       n += nadd;
       nm1 += (double)(int)nadd;
-      // T of an automatic flush of P adds (every flush but a call's first
-      // and its final partial one) and its divider were made one flush ahead
-      int T;
-      CsDiv cd;
-      if (GK_TPRED && nadd == P && Tpred >= 0) {
-        T = Tpred;
-        cd = cdpred;
-      } else {
-        T = __builtin_amdgcn_readfirstlane((int)(st.two_eps * nm1));
-        cd = make_csdiv(T);
-      }
-      Tpred = __builtin_amdgcn_readfirstlane((int)(st.two_eps * (nm1 + (double)P)));
-      cdpred = make_csdiv(Tpred);
+      const int T = __builtin_amdgcn_readfirstlane((int)(st.two_eps * nm1));
+      const CsDiv cd = make_csdiv(T);
       GK_MARK(L, 8);
       int nE;
       if constexpr (SMALL_CAP > 128)
@@ -4287,12 +4092,7 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
 #pragma unroll
       for (int r = 0; r < 2; ++r) {
         v[r] = L.tv[pidx(lane + 64 * r)];
-#if GK_GD16
-        const uint32_t w = L.tgd[lane + 64 * r];
-        gd[r] = make_int2(gd_g(w), gd_d(w));
-#else
         gd[r] = L.tgd[lane + 64 * r];
-#endif
       }
 #pragma unroll
       for (int r = 0; r < 2; ++r)
@@ -4311,11 +4111,6 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
     for (int i = 0; i < GK_PROF_NSEC; ++i) atomicAdd(&gk_prof_acc[i], L.prof[i]);
 #endif
 }
-
-#ifndef GK_HALF_WAVES
-#define GK_HALF_WAVES 4  // min waves per SIMD for k_ingest_half (128 VGPRs)
-#endif
-#include "gk_half.inc"
 
 // ===========================================================================
 // k_merge: GKArray.merge (gk:111-154) and merge_compress(entries), stream by
@@ -4967,24 +4762,7 @@ static hipError_t launch_ingest_small(const GKState& st, const double* x, const 
   const int pace = nstat > 0 && grid >= 4 * (int64_t)nstat && grid >= 8 * GK_WORK_PARTS ? 1 : 0;
   static const int lag = getenv("GK_FS_LAG") ? atoi(getenv("GK_FS_LAG")) : GK_FS_LAG_DEFAULT;
   if (list) return hipErrorInvalidValue;  // class 0 over every stream only
-  // GK_HALF=1: two streams per wave (k_ingest_half, experiment)
-  static const bool half = getenv("GK_HALF") && atoi(getenv("GK_HALF")) != 0;
-  if (half) {
-    int hocc = 0;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&hocc, k_ingest_half<false>, 64, 0);
-    if (hocc <= 0) hocc = 1;
-    int64_t hgrid = (int64_t)num_cu() * hocc;
-    if (hgrid > (count + 1) / 2) hgrid = (count + 1) / 2;
-    if (hgrid < 1) hgrid = 1;
-    if (nstat > hgrid) nstat = (int)hgrid;
-    const int hpace = nstat > 0 && hgrid >= 4 * (int64_t)nstat && hgrid >= 8 * GK_WORK_PARTS ? 1 : 0;
-    if (nstat > 0)
-      hipLaunchKernelGGL((k_ingest_half<true>), dim3((unsigned)hgrid), dim3(64), 0, stream, st, x, offs, count,
-                         force, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode, work, nstat, hpace, lag);
-    else
-      hipLaunchKernelGGL((k_ingest_half<false>), dim3((unsigned)hgrid), dim3(64), 0, stream, st, x, offs, count,
-                         force, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode, work, nstat, hpace, lag);
-  } else if (nstat > 0)
+  if (nstat > 0)
     hipLaunchKernelGGL((k_ingest_small<VPL, true>), dim3((unsigned)grid), dim3(64), 0, stream, st, x, offs, count,
                        force, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode, work, nstat, pace, lag);
   else

@@ -4,7 +4,9 @@ with backend "nccl"; gloo on CPU for tests).
 Two ways streams meet several GPUs:
 
 * **stream-sharded** -- every stream lives on exactly one rank
-  (``stream_range``); ranks never talk on the data path (weak scaling).
+  (``stream_range``, or ``balanced_assignment`` by length); ranks never talk
+  on the data path.  bench.py splits the metric's ONE batch this way (strong
+  scaling: the node's work is fixed as N grows).
 * **row-sharded** -- every rank sketched a slice of the rows of the SAME
   streams; the sketches are combined with the reference's left fold
   ``sk_0.merge(sk_1) ... .merge(sk_{N-1})`` (gk:111-154).  ``merge_row_shards``

@@ -150,7 +150,10 @@ def test_ingest_with_host_chains_returns_before_the_kernel(gpu_device, monkeypat
     total = time.perf_counter() - t0
     assert busy, "the call returned after the device work had finished (%.1f ms, total %.1f ms)" % (
         dt * 1e3, total * 1e3)
+    # taken == 1 only if the worker's walk was the one applied: a join that
+    # timed out (20 s) and fell back to the device walk reports 0
     assert ss.host_chains_taken == 1
+    assert total < 10.0, "the call's work took %.1f s (the host-chain join is bounded at 20 s)" % total
     o = OracleSet(64, 0.001)
     o.ingest(np.concatenate(seqs), offs)
     ost = o.stats()

@@ -4,9 +4,14 @@ waves), beside the one-wave-per-stream class-0 launch, which skips them.
 
 Parity bar: every stream's table, pending values, n/min/max/sum/avg and the
 fused quantiles bit-identical to the C oracle and to the same calls with the
-path switched off (GK_WG=0), over several calls (with GK_WG_PRESORT=1 the
-presort workspace exists from the second call on, so the path engages then;
-by default the batches are not presorted and the path engages at once) with pending values carried
+path switched off (GK_WG=0), over several calls, in the three presort
+modes: the default (GK_WG_PRESORT=1, GK_WG_CONC=1: the register presort runs
+BESIDE the workgroups, which rank batches unsorted until it has finished and
+always rank a call's first batch -- the one holding pre-call pending values --
+unsorted), the presort ahead of the workgroups (GK_WG_CONC=0) and no presort
+(GK_WG_PRESORT=0: every batch ranked among its gaps' members); the presort
+workspace is sized from the previous call's need, so presorted batches appear
+from the second call on.  Pending values are carried
 between calls, ties, signed zeros, and one adversarial (descending) long
 stream whose table outgrows the 2048 class inside k_ingest_wg (promoted and
 re-run in the next class).  GK_WG_TRACE=1 shows on stderr how many streams
@@ -60,17 +65,20 @@ def run(dev, monkeypatch, env, calls):
     return ss, res
 
 
-@pytest.mark.parametrize("presort", ["0", "1"])
-def test_wg_streams_match_oracle_and_one_wave_path(gpu_device, monkeypatch, capfd, presort):
-    """presort 0 (default): k_ingest_wg ranks unsorted batches among their
-    gaps' members (and sorts a batch with a crowded gap: the descending
-    stream's batches all fall below the table); 1: presorted batches."""
+@pytest.mark.parametrize("presort,conc", [("1", "1"), ("1", "0"), ("0", "1")])
+def test_wg_streams_match_oracle_and_one_wave_path(gpu_device, monkeypatch, capfd, presort, conc):
+    """presort 1, conc 1 (the default): presorted batches from the presort
+    running beside the workgroups; conc 0: the presort ahead of them;
+    presort 0: k_ingest_wg ranks every batch among its gaps' members (and
+    sorts a batch with a crowded gap: the descending stream's batches all
+    fall below the table)."""
     calls = batches(5)
-    ss, res = run(gpu_device, monkeypatch, {"GK_WG": "1", "GK_WG_TRACE": "1", "GK_WG_PRESORT": presort}, calls)
+    ss, res = run(gpu_device, monkeypatch, {"GK_WG": "1", "GK_WG_TRACE": "1", "GK_WG_PRESORT": presort,
+                                            "GK_WG_CONC": conc}, calls)
     err = capfd.readouterr().err
     took = [int(m) for m in re.findall(r"k_ingest_wg: (\d+) stream", err)]
     assert took and max(took) > 0, "k_ingest_wg took no stream: %r" % err[-2000:]
-    ss_off, res_off = run(gpu_device, monkeypatch, {"GK_WG": "0", "GK_WG_PRESORT": "0"}, calls)
+    ss_off, res_off = run(gpu_device, monkeypatch, {"GK_WG": "0", "GK_WG_PRESORT": "0", "GK_WG_CONC": "1"}, calls)
     o = OracleSet(200, EPS)
     for (q, offs), (q_off, _), seqs in zip(res, res_off, calls):
         o.ingest(np.concatenate(seqs), offs)

@@ -1,6 +1,6 @@
 """Per-launch SQ counters of k_ingest_small from scripts/pmc_sq.sh output dirs,
 per flush (1e7 flushes per cfg3 launch) and LDS share.  Usage: sq_summary.py TAG [TAG2 ...]
-(KRX in the environment: another kernel name, e.g. k_ingest_half)"""
+(KRX in the environment: another kernel name, e.g. k_ingest_wg)"""
 import csv
 import glob
 import os
