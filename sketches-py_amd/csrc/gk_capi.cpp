@@ -287,11 +287,11 @@ void poll(gk_set* h, bool block) {
     fprintf(stderr, "[gk] k_ingest_wg: %d stream(s)\n", h->h_ctr[GK_CTR_WORDS]);
   const int32_t fatal = h->h_ctr[GK_CTR_FATAL];
   if (fatal > h->fatal_seen && h->sticky == GK_OK) {
-    char buf[256];
+    char buf[512];
     snprintf(buf, sizeof(buf),
              "%d stream(s) (largest id %d) outgrew every table capacity class (largest %d entries), found no "
              "free slot, or passed the per-stream count limit 2*eps*(n-1) <= 2^30: their values of that call "
-             "were not added",
+             "were not added (past the last flush that fitted the smallest class, if one did)",
              fatal - h->fatal_seen, h->h_ctr[GK_CTR_FATAL + 1], h->st.cap[h->st.nclass - 1]);
     h->sticky = GK_E_OVERFLOW;
     h->sticky_msg = buf;
@@ -299,7 +299,8 @@ void poll(gk_set* h, bool block) {
   h->fatal_seen = fatal;
 }
 
-int promote_rounds(gk_set* h, const double* x, const int64_t* offs, int force, const GKQuery& q, hipStream_t s);
+int promote_rounds(gk_set* h, const double* x, const int64_t* offs, int force, const GKQuery& q, hipStream_t s,
+                   bool fresh = false);
 int mark_done(gk_set* h, hipStream_t s);
 
 // Start of a call's device work: ONE memset zeroes every per-call counter
@@ -708,7 +709,15 @@ int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s) {
   // chains start at once), then on `s` the short streams' chains (k_stats,
   // unless the small-class launch walks them) and the presort of the long
   // streams' flush batches
-  HIP_TRY(gk_launch_stats(h->st, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->ps, s));
+  HIP_TRY(gk_launch_stats(h->st, offs, h->d_long_list, h->d_long_count, s));
+  // k_long_prep sorts the list and plans the presort / workgroups, which the
+  // launches on `s` use -- unless the small-class launch carries the stats
+  // role (P <= 128: no presort, no workgroups) and no host chain is picked
+  // from the sorted list: then nothing on `s` reads it before the join, and
+  // it runs on `aux` ahead of k_stats_long (off the ingest's critical path)
+  const bool prep_aux = stats_fused(h) && !(h->hc_min > 0);
+  if (!prep_aux)
+    HIP_TRY(gk_launch_long_prep(h->st, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->ps, s));
   // the longest chains to host cores: k_hc_prep picks them (k_stats_long
   // skips them) ahead of the fork, so that `aux` holds nothing but
   // k_stats_long and its waves reach the CUs before the ingest grid of this
@@ -736,6 +745,8 @@ int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s) {
   HIP_TRY(hipEventRecord(h->ev_fork, s));
   HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_fork, 0));
   h->forked = true;
+  if (prep_aux)
+    HIP_TRY(gk_launch_long_prep(h->st, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->ps, h->aux));
   HIP_TRY(gk_launch_stats_long(h->st, x, offs, h->d_long_list, h->d_long_n, h->d_long_count,
                                hc_on ? h->d_hc_count : nullptr, h->aux));
   h->hc_active = hc_on;  // (stats_join hands the picked chains to the worker)
@@ -795,7 +806,9 @@ int stats_join(gk_set* h, hipStream_t s, const GKQuery& q) {
     HIP_TRY(gk_launch_hc_fallback(h->st, h->hc_x, h->hc_offs, h->d_long_list, h->d_long_n, h->d_hc_count,
                                   h->d_hc_fail, s));
   }
-  HIP_TRY(gk_launch_query_list(h->st, h->d_long_list, h->d_long_count, q, s));
+  // (+ the _min/_max markers of the small-class launch's answers when it
+  // carried the stats role: its chains are final here)
+  HIP_TRY(gk_launch_query_list(h->st, h->d_long_list, h->d_long_count, q, stats_fused(h), s));
   return GK_OK;
 }
 
@@ -805,11 +818,20 @@ int stats_join(gk_set* h, hipStream_t s, const GKQuery& q) {
 // (k_promote_dev) and runs again there, at most once per class; a stream
 // with no class left is counted as fatal (reported by a later call).
 // Promotion rounds of a call: round r-1's overflow list moves one class up
-// on the device and runs again in its new class (round r).
-int promote_rounds(gk_set* h, const double* x, const int64_t* offs, int force, const GKQuery& q, hipStream_t stream) {
+// on the device and runs again in its new class (round r).  fresh: every
+// stream started the call in class 0 (gk_create / gk_reset, nothing promoted
+// since), so after r rounds no stream is above class r: round r re-runs
+// class r only (the launches of the classes above would find their re-run
+// lists empty).
+int promote_rounds(gk_set* h, const double* x, const int64_t* offs, int force, const GKQuery& q, hipStream_t stream,
+                   bool fresh) {
   const int R = h->st.nclass;
   GKPoolDev pool = pool_args(h);
+  bool ran = true;  // a launch ran in the previous round (round 0: class 0)
   for (int r = 1; r <= R; ++r) {
+    // (fresh: round r-1 re-ran class r-1 only; a class with no slots has no
+    // launch, and then round r has nothing to promote)
+    if (fresh && !ran) break;
     int32_t* rcnt = h->d_ctr + GK_CTR_RCNT + GK_MAX_CLASSES * r;  // zeroed at the start of the call
     pool.rcnt = rcnt;
     h->no_members = false;
@@ -819,7 +841,9 @@ int promote_rounds(gk_set* h, const double* x, const int64_t* offs, int force, c
       GK_TR("round %d: promoted", r);
     }
     if (r == R) break;  // the last promotion only counts what no class can hold
-    for (int c = r; c < R; ++c) {
+    ran = false;
+    for (int c = r; c < (fresh ? r + 1 : R); ++c) {
+      ran |= h->st.alloc[c] > 0;  // (launch_class launches nothing without slots)
       HIP_TRY(launch_class(h, c, x, offs, h->d_rerun[c], rcnt + c, r, force, q, stream));
       if (g_trace) {
         HIP_TRY(hipStreamSynchronize(stream));
@@ -834,6 +858,7 @@ int run_ingest(gk_set* h, const double* x, const int64_t* offs, int force, hipSt
                const GKQuery& q = GKQuery(), bool prio = false) {
   if (!offs) offs = h->d_zero_offs;
   const int R = h->st.nclass;
+  const bool fresh = h->no_members;  // (promote_rounds clears it)
   h->last.x = x;
   h->last.offs = offs;
   h->last.force = force;
@@ -873,7 +898,7 @@ int run_ingest(gk_set* h, const double* x, const int64_t* offs, int force, hipSt
   if (!h->no_members)
     for (int c = 1; c < R; ++c)
       HIP_TRY(launch_class(h, c, x, offs, h->d_list[c], h->d_ctr + GK_CTR_LCNT + c, 0, force, q, stream));
-  return promote_rounds(h, x, offs, force, q, stream);
+  return promote_rounds(h, x, offs, force, q, stream, fresh);
 }
 
 // Merge / explicit merge_compress at LDS capacity level 0, then the streams
@@ -1197,8 +1222,7 @@ int gk_reset(gk_set* h, void* stream) {
   // (k_reset puts every stream back in class 0: cls = slot = 0)
   // slots, member lists and re-run lists start over (FATAL stays cumulative:
   // a readback still in flight carries it)
-  HIP_TRY(hipMemsetAsync(h->d_ctr, 0, GK_CTR_FATAL * sizeof(int32_t), s));
-  HIP_TRY(gk_launch_reset(h->st, s));
+  HIP_TRY(gk_launch_reset(h->st, s, h->d_ctr));  // (+ counter words [0, GK_CTR_FATAL): no separate memset)
   h->no_members = true;
   return GK_OK;
 }

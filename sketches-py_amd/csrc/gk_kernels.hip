@@ -68,7 +68,7 @@ __device__ __forceinline__ GKBigProf& gk_big_prof() {
 #endif
 
 // quantile answers that are the stream's _min / _max while the stats role of
-// the launch may still be writing them (k_qfix replaces them afterwards)
+// the launch may still be writing them (the join, k_query_list, replaces them)
 #define GK_QMARK_MIN 0x7ff4000000000001LL  // quantile = _min of the stream (gk:182-183, 220)
 #define GK_QMARK_MAX 0x7ff4000000000002LL  // quantile = _max of the stream (gk:229)
 #define GK_KEEP_BIT 0x40000000
@@ -382,7 +382,9 @@ __global__ __launch_bounds__(1024) void k_long_prep(GKState st, const int64_t* _
     for (int i = t; i < cnt; i += 1024) list[i] = (int32_t)(key[i] & 0x7fffffffu);
     __syncthreads();
   }
-  for (int i = t; i < cnt; i += 1024) list_n[i] = st.n[list[i]];
+  // (the pre-call n from k_lengths' snapshot: with the stats role fused, this
+  // kernel runs beside the ingest launch, which rewrites st.n)
+  for (int i = t; i < cnt; i += 1024) list_n[i] = st.n0[list[i]];
   if (!list_ws) return;
   __syncthreads();
   // Presort plan (k_presort): every automatic flush of a listed class-0
@@ -1577,13 +1579,32 @@ __device__ __attribute__((noinline)) void wave_quantiles(const double* __restric
 // launch answers every stream before k_stats_long (running beside it) has
 // produced the final _min/_max of the long streams (gk:183, 220, 229); this
 // launch re-answers exactly those streams once it has joined.
-__global__ __launch_bounds__(64) void k_query_list(GKState st, const int32_t* __restrict__ list,
-                                                   const int32_t* __restrict__ count,
-                                                   const double* __restrict__ qs, int nq, int qmode,
-                                                   double* __restrict__ qout) {
-  const int lane = threadIdx.x;
+// The join of a fused ingest + query (one wave per block):
+//  * qfix (the small-class launch carried the stats role): an answer that is
+//    _min or _max (gk:182-183, gk:229) was written as a marker NaN while the
+//    stats role could still be writing them; now they are final.  One answer
+//    per thread (the grid covers S*nq; no loop: every load in flight at once).
+//  * the long streams (`list`), answered again from their final _min/_max
+//    (k_stats_long ran beside the ingest), one per wave.  (A long stream
+//    whose answer the qfix part also resolves gets the same bits from both.)
+__global__ __launch_bounds__(256) void k_query_list(GKState st, const int32_t* __restrict__ list,
+                                                    const int32_t* __restrict__ count,
+                                                    const double* __restrict__ qs, int nq, int qmode,
+                                                    double* __restrict__ qout, int qfix) {
+  const int lane = threadIdx.x & 63;
+  if (qfix) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < st.S * (int64_t)nq) {
+      const long long b = __double_as_longlong(qout[i]);
+      if (b == GK_QMARK_MIN || b == GK_QMARK_MAX) {
+        const int64_t s = i / nq;
+        qout[i] = b == GK_QMARK_MIN ? st.mn[s] : st.mx[s];
+      }
+    }
+  }
   const int cnt = *count;
-  for (int w = blockIdx.x; w < cnt; w += gridDim.x) {
+  const int wid = (int)(blockIdx.x * 4 + (threadIdx.x >> 6)), nwv = (int)(gridDim.x * 4);
+  for (int w = wid; w < cnt; w += nwv) {
     const int64_t s = list[w];
     const GKRec* tab = gk_table_ptr(st, s);
     wave_quantiles<2, 4>(&tab->v, &tab->g, &tab->d, st.E[s], st.n[s], st.mn[s], st.mx[s], st, qs, nq, qmode,
@@ -1646,6 +1667,9 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
   if (count_ptr) count = *count_ptr;
   const int64_t npri = prio ? max((int64_t)*prio_count - skip, (int64_t)0) : 0;
   const int64_t total = npri + count;
+  // blocks past the item count leave before the hand-out (the ones below it
+  // take every item): an empty or short re-run list costs no atomics
+  if ((int64_t)blockIdx.x >= total) return;
   auto grab = [&]() -> int64_t {
     unsigned long long v = 0;
     if (lane == 0) v = atomicAdd(work, 1ull);
@@ -1668,13 +1692,16 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
     int p = __builtin_amdgcn_readfirstlane(hv.pend);
     int E = __builtin_amdgcn_readfirstlane(hv.E);
     int64_t n = rfl64(hv.n);
-    const int64_t xo = rfl64(hv.xo);
+    const int64_t xo0 = rfl64(hv.xo);
     const int64_t xe = rfl64(hv.xe);
     const double smn = __longlong_as_double(rfl64(__double_as_longlong(hv.mn)));
     const double smx = __longlong_as_double(rfl64(__double_as_longlong(hv.mx)));
     if (wn < total) gk_hdr_issue(hv, st, offs, sid(wn));
     w = wn;
     if (scls != lcls) continue;  // in another class: handled by that class's launch
+    // a promoted stream continues from value n - n0 of the call (the flushes
+    // its smaller class made before overflowing are committed: k_ingest_small)
+    const int64_t xo = xo0 + ((lcls > 0 && x) ? n - rfl64(st.n0[s]) : 0);
     const int64_t Lx = xe - xo;
     if (prio && !from_prio && Lx > GK_STATS_LONG) continue;  // taken from `prio`
 
@@ -2655,6 +2682,7 @@ __global__ __launch_bounds__(64) void k_ingest_big(GKState st, const double* __r
   const int P = st.P;
   const BigBuf B = big_buf(ws + (size_t)blockIdx.x * ws_bytes, cap, gk_big_np(P));
   if (count_ptr) count = *count_ptr;
+  if ((int64_t)blockIdx.x >= count) return;  // (the blocks below the count take every item)
   for (;;) {
     unsigned long long wv = 0;
     if (lane == 0) wv = atomicAdd(work, 1ull);
@@ -2665,7 +2693,9 @@ __global__ __launch_bounds__(64) void k_ingest_big(GKState st, const double* __r
     int p = __builtin_amdgcn_readfirstlane(st.pend[s]);
     int E = __builtin_amdgcn_readfirstlane(st.E[s]);
     int64_t n = rfl64(st.n[s]);
-    const int64_t xo = rfl64(offs[s]);
+    // a promoted stream continues from value n - n0 of the call (the flushes
+    // its smaller class made before overflowing are committed: k_ingest_small)
+    const int64_t xo = rfl64(offs[s]) + ((lcls > 0 && x) ? n - rfl64(st.n0[s]) : 0);
     const int64_t Lx = rfl64(offs[s + 1]) - xo;
     if (Lx <= 0 && !((force == 1 && p > 0) || (force == 2 && n > 0)) && !qs) continue;
     // a stream past the per-stream count limit is refused like an overflow,
@@ -3755,7 +3785,7 @@ __device__ __attribute__((noinline)) double small_quantiles(SmallLDS<VPL>& L, in
 // ingest hand-out.  Batches of 64 streams are handed out through `swork`.
 // Streams longer than GK_STATS_LONG are k_stats_long's (listed beforehand by
 // the lengths-only k_lengths).  The ingest waves do not read _min/_max: a fused
-// query that needs them writes a marker that k_qfix resolves after the launch.
+// query that needs them writes a marker that the join (k_query_list) resolves.
 #ifndef GK_FS_DEPTH
 #define GK_FS_DEPTH 2  // chunks of 8 values in flight per lane
 #endif
@@ -3888,14 +3918,6 @@ __device__ __forceinline__ void fused_stats_role(const GKState& st, const double
 }
 
 // fused-stats launches: quantiles that are _min / _max (markers) resolved
-__global__ void k_qfix(GKState st, double* __restrict__ out, int nq) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= st.S * (int64_t)nq) return;
-  const long long b = __double_as_longlong(out[i]);
-  if (b == GK_QMARK_MIN) out[i] = st.mn[i / nq];
-  else if (b == GK_QMARK_MAX) out[i] = st.mx[i / nq];
-}
-
 // FS: the launch carries the stats role (nstat > 0): _min/_max are not final
 // during it, so the header prefetch skips them and fused quantiles use markers.
 // Class 0 over every stream only (promoted streams are skipped: their class's
@@ -4040,6 +4062,7 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
       else
         nE = flush_small<VPL, 2>(L, E, xv, cnt, T, cd, lane, prefetch);
       if (nE < 0) {
+        n -= nadd;  // (this flush is not made here: the state stays that of the last flush that fitted)
         ok = false;
         break;
       }
@@ -4068,9 +4091,33 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
       p += (int)rem;
       n += rem;
     }
+    // the table (E <= 127: two records per lane, all LDS reads before the
+    // 16-byte stores) and the header words
+    auto write_back = [&]() {
+      double v[2];
+      int2 gd[2];
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        v[r] = L.tv[pidx(lane + 64 * r)];
+        gd[r] = L.tgd[lane + 64 * r];
+      }
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+        if (lane + 64 * r < E) ((int4*)tab)[lane + 64 * r] = make_int4(__double2loint(v[r]), __double2hiint(v[r]), gd[r].x, gd[r].y);
+      if (lane == 0) {
+        st.n[s] = n;
+        st.E[s] = E;
+        st.pend[s] = p;
+      }
+    };
     if (!ok) {
-      // nothing was written back: the stream keeps its pre-call state and is
-      // re-run by the host after promotion to the next capacity class
+      // The flush that outgrew the class is not made.  The flushes before it
+      // are committed (table, n, no pending value): the stream is promoted to
+      // the next class on the device and continues there from value n - n0
+      // of this call (st.n0: the pre-call n, k_lengths) instead of re-running
+      // the whole call.  Without a flush in this call the pre-call state
+      // stays as it was.
+      if (flushed) write_back();
       if (lane == 0) {
         const int k = atomicAdd(ovf_count, 1);
         ovf_list[k] = (int32_t)s;
@@ -4085,24 +4132,7 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
         if (q0 + lane < nq) qout[s * (int64_t)nq + q0 + lane] = r;
       }
     }
-    {
-      // E <= 127: two records per lane, all LDS reads before the 16-byte stores
-      double v[2];
-      int2 gd[2];
-#pragma unroll
-      for (int r = 0; r < 2; ++r) {
-        v[r] = L.tv[pidx(lane + 64 * r)];
-        gd[r] = L.tgd[lane + 64 * r];
-      }
-#pragma unroll
-      for (int r = 0; r < 2; ++r)
-        if (lane + 64 * r < E) ((int4*)tab)[lane + 64 * r] = make_int4(__double2loint(v[r]), __double2hiint(v[r]), gd[r].x, gd[r].y);
-    }
-    if (lane == 0) {
-      st.n[s] = n;
-      st.E[s] = E;
-      st.pend[s] = p;
-    }
+    write_back();
     wsync<false>();
     GK_MARK(L, 9);
   }
@@ -4503,8 +4533,11 @@ __global__ __launch_bounds__(64) void k_merge(MergeArgs a) {
 // ===========================================================================
 // state movement
 // ===========================================================================
-__global__ void k_reset(GKState st) {
+// ctr (gk_reset): the set's slot and member-list counters start over too
+// (words [0, GK_CTR_FATAL); FATAL stays cumulative)
+__global__ void k_reset(GKState st, int32_t* __restrict__ ctr) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (ctr && s < GK_CTR_FATAL) ctr[s] = 0;
   if (s >= st.S) return;
   st.n[s] = 0;
   st.E[s] = 0;
@@ -4768,10 +4801,6 @@ static hipError_t launch_ingest_small(const GKState& st, const double* x, const 
   else
     hipLaunchKernelGGL((k_ingest_small<VPL, false>), dim3((unsigned)grid), dim3(64), 0, stream, st, x, offs, count,
                        force, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode, work, nstat, pace, lag);
-  if (nstat > 0 && q.qs && q.nq > 0) {
-    const int64_t tot = st.S * (int64_t)q.nq;
-    hipLaunchKernelGGL(k_qfix, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, st, q.out, q.nq);
-  }
   return hipGetLastError();
 }
 
@@ -4830,8 +4859,8 @@ hipError_t gk_launch_ingest_wg(const GKState& st, const double* x, const int64_t
   return hipGetLastError();
 }
 
-hipError_t gk_launch_stats(const GKState& st, const int64_t* offs, int32_t* long_list, int64_t* long_n,
-                           int32_t* long_count, const GKPresort& ps, hipStream_t stream) {
+hipError_t gk_launch_stats(const GKState& st, const int64_t* offs, int32_t* long_list, int32_t* long_count,
+                           hipStream_t stream) {
   if (st.S <= 0) return hipSuccess;
   const int64_t grid = (st.S + 255) / 256;
   // the long-stream list first (k_lengths, a few us), so that the caller can
@@ -4839,6 +4868,12 @@ hipError_t gk_launch_stats(const GKState& st, const int64_t* offs, int32_t* long
   // critical path of a Zipf batch -- before the short streams' chains
   // (gk_launch_stats_short) run on this stream
   hipLaunchKernelGGL(k_lengths, dim3((unsigned)grid), dim3(256), 0, stream, st, offs, long_list, long_count);
+  return hipGetLastError();
+}
+
+hipError_t gk_launch_long_prep(const GKState& st, const int64_t* offs, int32_t* long_list, int64_t* long_n,
+                               int32_t* long_count, const GKPresort& ps, hipStream_t stream) {
+  if (st.S <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_long_prep, dim3(1), dim3(1024), 0, stream, st, offs, long_list, long_n,
                      (const int32_t*)long_count, ps.list_ws, ps.list_b0, ps.ws_cap, ps.ws_need, ps.wg_count,
                      ps.wg_presort);
@@ -4923,10 +4958,13 @@ hipError_t gk_launch_hc_fallback(const GKState& st, const double* x, const int64
 }
 
 hipError_t gk_launch_query_list(const GKState& st, const int32_t* list, const int32_t* count, const GKQuery& q,
-                                hipStream_t stream) {
+                                bool qfix, hipStream_t stream) {
   if (st.S <= 0 || !q.qs || q.nq <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_query_list, dim3((unsigned)(num_cu() * 4)), dim3(64), 0, stream, st, list, count, q.qs, q.nq,
-                     q.mode, q.out);
+  // (4 waves per block: num_cu() blocks = 4 waves per CU for the list; the
+  // marker fix needs one thread per answer)
+  const int64_t grid = std::max<int64_t>(num_cu(), qfix ? (st.S * (int64_t)q.nq + 255) / 256 : 0);
+  hipLaunchKernelGGL(k_query_list, dim3((unsigned)grid), dim3(256), 0, stream, st, list, count, q.qs, q.nq,
+                     q.mode, q.out, qfix ? 1 : 0);
   return hipGetLastError();
 }
 
@@ -4981,10 +5019,10 @@ hipError_t gk_launch_rtab(const GKState& st, hipStream_t stream) {
   return hipGetLastError();
 }
 
-hipError_t gk_launch_reset(const GKState& st, hipStream_t stream) {
-  if (st.S <= 0) return hipSuccess;
-  const int64_t grid = (st.S + 255) / 256;
-  hipLaunchKernelGGL(k_reset, dim3((unsigned)grid), dim3(256), 0, stream, st);
+hipError_t gk_launch_reset(const GKState& st, hipStream_t stream, int32_t* ctr) {
+  if (st.S <= 0 && !ctr) return hipSuccess;
+  const int64_t grid = (std::max<int64_t>(st.S, GK_CTR_FATAL) + 255) / 256;
+  hipLaunchKernelGGL(k_reset, dim3((unsigned)grid), dim3(256), 0, stream, st, ctr);
   return hipGetLastError();
 }
 

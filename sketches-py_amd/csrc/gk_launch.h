@@ -95,9 +95,13 @@ struct GKPresort {
 hipError_t gk_launch_ingest_wg(const GKState& st, const double* x, const int64_t* offs, const int32_t* long_list,
                                const int32_t* wg_count, int lcls, int force, int32_t* ovf_count, int32_t* ovf_list,
                                unsigned long long* work, const GKPresort& ps, hipStream_t stream);
-// the long-stream list + pre-call n (k_lengths), then k_long_prep
-hipError_t gk_launch_stats(const GKState& st, const int64_t* offs, int32_t* long_list, int64_t* long_n,
-                           int32_t* long_count, const GKPresort& ps, hipStream_t stream);
+// the long-stream list + every stream's pre-call n (k_lengths)
+hipError_t gk_launch_stats(const GKState& st, const int64_t* offs, int32_t* long_list, int32_t* long_count,
+                           hipStream_t stream);
+// the long list sorted longest first, the listed streams' pre-call n, the
+// presort plan and k_ingest_wg's stream count (k_long_prep)
+hipError_t gk_launch_long_prep(const GKState& st, const int64_t* offs, int32_t* long_list, int64_t* long_n,
+                               int32_t* long_count, const GKPresort& ps, hipStream_t stream);
 // gk:52-59 chains of the streams up to GK_STATS_LONG values (k_stats_short; the
 // long ones are k_stats_long's), when class 0 is not the small class
 hipError_t gk_launch_stats_short(const GKState& st, const double* x, const int64_t* offs, hipStream_t stream);
@@ -139,12 +143,16 @@ hipError_t gk_launch_hc_wait(const unsigned long long* flag, unsigned long long 
 hipError_t gk_launch_hc_fallback(const GKState& st, const double* x, const int64_t* offs, const int32_t* long_list,
                                  const int64_t* long_n, const int32_t* hc_count, const int32_t* fail,
                                  hipStream_t stream);
-// quantiles of the listed streams from their committed tables (after the join)
+// quantiles of the listed streams from their committed tables (after the
+// join); qfix: also resolve the _min/_max markers of a small-class launch
+// that carried the stats role (every stream's answers)
 hipError_t gk_launch_query_list(const GKState& st, const int32_t* list, const int32_t* count, const GKQuery& q,
-                                hipStream_t stream);
+                                bool qfix, hipStream_t stream);
 size_t gk_merge_lds_bytes(int cap, int pmax);
 hipError_t gk_launch_merge(const MergeArgsHost& h, hipStream_t stream);
-hipError_t gk_launch_reset(const GKState& st, hipStream_t stream);
+// every stream back to an empty sketch in class 0; ctr: also zero the set's
+// counter words [0, GK_CTR_FATAL) (slots used, member-list lengths)
+hipError_t gk_launch_reset(const GKState& st, hipStream_t stream, int32_t* ctr = nullptr);
 // fills st.rtab (reciprocals 1.0/k, k < st.rtab_n)
 hipError_t gk_launch_rtab(const GKState& st, hipStream_t stream);
 hipError_t gk_launch_export(const GKState& st, const int64_t* offs, double* v, int32_t* g, int32_t* d,
@@ -166,26 +174,29 @@ hipError_t gk_launch_promote(const GKState& st, const int32_t* list, int64_t cou
 //   persistent:  [0..3] slots used per class, [4..7] member-list lengths,
 //                [12] streams with no class left, [13] the largest such id
 //   per call (zeroed by ONE memset at the start of every call, from word
-//   GK_CTR_CALL to GK_CALL_BYTES):  [14] deferred streams, [15] long-stream
-//   list length, [16 + 4r + c] round r's re-run list length of class c,
-//   [40 + r] round r's overflow count, then (byte GK_CALL_WORK) the launches'
-//   stream hand-out counters.
+//   GK_CTR_CALL -- 16, a 64-byte boundary: one fill -- to GK_CALL_BYTES):
+//   [16] deferred streams, [17] long-stream list length, [20 + 4r + c] round
+//   r's re-run list length of class c, [40 + r] round r's overflow count,
+//   then (byte GK_CALL_WORK) the launches' stream hand-out counters.
 // The host reads words [0, GK_CTR_WORDS) back after every call.
 #define GK_CTR_USED 0
 #define GK_CTR_LCNT 4
 #define GK_CTR_FATAL 12   // [12] count, [13] largest such stream id
-#define GK_CTR_DEFER 14   // streams whose class had no free slot this call (re-run by the host later)
-#define GK_CTR_LONG 15    // streams longer than GK_STATS_LONG values (k_stats)
-#define GK_CTR_RCNT 16    // [16 + 4*round + class]
+#define GK_CTR_DEFER 16   // streams whose class had no free slot this call (re-run by the host later)
+#define GK_CTR_LONG 17    // streams longer than GK_STATS_LONG values (k_stats)
+#define GK_CTR_RCNT 20    // [20 + 4*round + class]
 #define GK_CTR_OVFC 40    // [40 + round]
 #define GK_CTR_BADPEND 48 // gk_import: streams with an unreachable pending count
 #define GK_CTR_WG 50      // k_ingest_wg's stream count this call (k_long_prep)
 #define GK_CTR_PSDONE 51  // k_presort_reg's finished waves this call (k_ingest_wg beside it)
-#define GK_CTR_WORDS 16
-#define GK_CTR_CALL 14
+#define GK_CTR_WORDS 18
+#define GK_CTR_CALL 16
 #define GK_CALL_WORK 256                          // bytes: the small-class launch's GK_WORK_BYTES, then
 #define GK_CALL_SLOTS 16                          //   16 counters of 128 bytes for the other launches
 #define GK_CALL_BYTES (GK_CALL_WORK + GK_WORK_BYTES + GK_CALL_SLOTS * 128)
+static_assert(GK_CTR_RCNT + 4 * (GK_MAX_CLASSES + 1) <= GK_CTR_OVFC, "re-run counts fit below the overflow counts");
+static_assert(GK_CTR_PSDONE < GK_CALL_WORK / 4, "counters fit below the hand-out block");
+static_assert((GK_CTR_CALL * 4) % 64 == 0 && (GK_CALL_BYTES - GK_CTR_CALL * 4) % 16 == 0, "aligned per-call memset");
 struct GKPoolDev {
   int32_t* ctr;
   int32_t* rcnt;  // this round's re-run list lengths (one per class)
