@@ -1,3 +1,7 @@
+"""One bench step's kernel timeline from a rocprofv3 --kernel-trace CSV: every
+dispatch between two k_reset launches (start offset, duration, gap to the
+previous end, queue, name) and the step's non-ingest kernel time.
+Usage: step_timeline.py <run_kernel_trace.csv>"""
 import csv, sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r['Start_Timestamp']))
