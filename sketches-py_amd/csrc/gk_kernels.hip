@@ -63,8 +63,34 @@ __device__ __forceinline__ GKBigProf& gk_big_prof() {
       p_.t = t_;                                             \
     }                                                        \
   } while (0)
+// k_ingest_wg, per wave (profiling builds): every wave's lane 0 adds the
+// cycles since its previous mark to [wave][point], so that each stretch of a
+// flush is split into its work and its barrier wait, wave by wave
+// (tools/prof_sections.py --workload wg --per-wave)
+#define GK_WP_N 16
+#define GK_WP_W 8
+__device__ unsigned long long gk_wprof_acc[GK_WP_W][GK_WP_N];
+struct GKWaveProf {
+  unsigned long long acc[GK_WP_W][GK_WP_N];
+  uint32_t t[GK_WP_W];
+};
+__device__ __forceinline__ GKWaveProf& gk_wave_prof() {
+  __shared__ GKWaveProf p;
+  return p;
+}
+#define GK_WMARK(pt)                                                   \
+  do {                                                                 \
+    if ((threadIdx.x & 63) == 0 && (threadIdx.x >> 6) < GK_WP_W) {     \
+      GKWaveProf& p_ = gk_wave_prof();                                 \
+      const int w_ = threadIdx.x >> 6;                                 \
+      const uint32_t t_ = gk_cycles();                                 \
+      p_.acc[w_][pt] += (uint32_t)(t_ - p_.t[w_]);                     \
+      p_.t[w_] = t_;                                                   \
+    }                                                                  \
+  } while (0)
 #else
 #define GK_BMARK(sec) do { } while (0)
+#define GK_WMARK(pt) do { } while (0)
 #endif
 
 // quantile answers that are the stream's _min / _max while the stats role of
@@ -1882,7 +1908,7 @@ struct WgLDS {
   double tv[2][GK_WG_CAP];
   int32_t tg[2][GK_WG_CAP];
   int32_t td[2][GK_WG_CAP];
-  uint32_t gpk[2][GK_WG_CAP + 1];  // per gap: count, then (member base << 16) | out base; by table parity
+  alignas(16) uint32_t gpk[2][GK_WG_CAP + 4];  // per gap: count, then (member base << 16) | out base; by table parity
   int32_t gk[GK_WG_CAP + 1];    // per entry: absorbed count | KEEP bit
   int32_t gdel[GK_WG_CAP + 1];  // per entry: G, then G + d - 1
   double sv[GK_WG_PMAX];        // sort area of a batch with a crowded gap
@@ -1891,8 +1917,24 @@ struct WgLDS {
   uint32_t wsum[GK_WG_WAVES];   // the scan's wave totals
   int psflag_pub[2];            // k_ingest_wg: the presort-done flag thread 0 saw, by flush parity
   int32_t xdone[GK_WG_WAVES], xc[GK_WG_WAVES];  // the carry walk's wave-boundary states
+  alignas(16) int32_t xall[GK_WG_WAVES];  // per wave: every lane's carry-in resolved (the walk's vote)
+  alignas(16) int32_t xbig[GK_WG_WAVES];  // per wave: a gap with GK_WG_RANK_MAX members or more
   uint32_t total;
 };
+
+// AND / OR over the workgroup of a per-wave flag (each wave's lane 0 has
+// stored it in f[w] before a plain barrier): two 16-byte LDS reads, where
+// __syncthreads_and / _or are a workgroup reduction with barriers of their own
+__device__ __forceinline__ int wg_flags_all(const int32_t* f) {
+  static_assert(GK_WG_WAVES == 8, "two int4 reads");
+  const int4 a = *(const int4*)f, b = *(const int4*)(f + 4);
+  return a.x & a.y & a.z & a.w & b.x & b.y & b.z & b.w;
+}
+__device__ __forceinline__ int wg_flags_any(const int32_t* f) {
+  static_assert(GK_WG_WAVES == 8, "two int4 reads");
+  const int4 a = *(const int4*)f, b = *(const int4*)(f + 4);
+  return a.x | a.y | a.z | a.w | b.x | b.y | b.z | b.w;
+}
 
 // values q = t + GK_WG_T * r of a batch of cnt in ascending (value, insertion
 // index) order: Python's stable sorted() of gk:71-72
@@ -1948,6 +1990,8 @@ __device__ __forceinline__ void wg_sort(WgLDS& L, double (&xv)[GK_WG_VPT], int c
 #ifndef GK_WG_RK_UNROLL
 #define GK_WG_RK_UNROLL 4
 #endif
+// KM: table entries per thread, >= ceil(E / GK_WG_T) (2 up to 1024 entries)
+template <int KM>
 __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG_VPT], const int cnt,
                         const int T, const int t, bool sorted) {
   const int lane = t & 63, w = t >> 6;
@@ -1962,13 +2006,13 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
   // now for the next flush (no zeroing pass + barrier before the atomics)
   uint32_t* __restrict__ gpk = L.gpk[cur];
   {
-    uint32_t* __restrict__ gz = L.gpk[cur ^ 1];
-    for (int j = t; j <= GK_WG_CAP; j += GK_WG_T) gz[j] = 0u;
+    uint4* __restrict__ gz = (uint4*)L.gpk[cur ^ 1];
+    for (int j = t; j < (GK_WG_CAP + 4) / 4; j += GK_WG_T) gz[j] = make_uint4(0u, 0u, 0u, 0u);
   }
   // this thread's block of entries for the carry walk below: their g, d (and
   // those of the entries either side) read now, under the search; only the
   // member counts wait for the atomics
-  constexpr int KM = GK_WG_KMAX;
+  static_assert(KM >= 1 && KM <= GK_WG_KMAX, "entries per thread");
   const int K = (E + GK_WG_T - 1) / GK_WG_T;
   const int j0 = t * K;
   const int jend = min(j0 + K, E);
@@ -1986,6 +2030,7 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
   const bool nx = has && jend < E;  // the entry after this block (the last entry's removal test)
   const int gnx = nx ? tg[jend] : 0, dnx = nx ? td[jend] : 0;
   const int gp_ = (has && t > 0) ? tg[j0 - 1] : 0, dp_ = (has && t > 0) ? td[j0 - 1] : 0;  // the entry before
+  GK_WMARK(1);  // setup: zeroing, the entries' g/d loads issued
   // ---- gap = #entries <= x (gk:93), branch-free over the +inf-padded table
   int xg[GK_WG_VPT];
   uint32_t slot[GK_WG_VPT];  // an unsorted value's member slot in its gap
@@ -2005,20 +2050,35 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
       for (int j = t; j <= E; j += GK_WG_T) gpk[j] = 0u;
       __syncthreads();
     }
+    GK_WMARK(2);  // gap search
     bool big = false;
+    if (sorted) {
+      // (no slot needed: no-return atomics)
 #pragma unroll
-    for (int r = 0; r < GK_WG_VPT; ++r) {
-      slot[r] = 0;
-      if (t + GK_WG_T * r < cnt) {
-        slot[r] = atomicAdd(&gpk[xg[r]], 1u);
-        big |= slot[r] >= GK_WG_RANK_MAX;
+      for (int r = 0; r < GK_WG_VPT; ++r)
+        if (t + GK_WG_T * r < cnt) (void)atomicAdd(&gpk[xg[r]], 1u);
+    } else {
+#pragma unroll
+      for (int r = 0; r < GK_WG_VPT; ++r) {
+        slot[r] = 0;
+        if (t + GK_WG_T * r < cnt) {
+          slot[r] = atomicAdd(&gpk[xg[r]], 1u);
+          big |= slot[r] >= GK_WG_RANK_MAX;
+        }
       }
     }
     if (sorted) {
+      GK_WMARK(3);  // count atomics (issued)
       __syncthreads();
+      GK_WMARK(4);  // count barrier (atomics drained + wait)
       break;
     }
-    if (!__syncthreads_or(big ? 1 : 0)) break;
+    {
+      const bool wbig = __builtin_amdgcn_ballot_w64(big) != 0;
+      if (lane == 0) L.xbig[w] = wbig ? 1 : 0;
+      __syncthreads();
+      if (!wg_flags_any(L.xbig)) break;  // (xbig is written again only after the sort's barriers)
+    }
     GK_BMARK(2);
     wg_sort(L, xv, cnt, t);  // a crowded gap: sort, then search again
     sorted = true;
@@ -2080,12 +2140,18 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
       }
       if (__builtin_amdgcn_ballot_w64(nkn) == 0) break;
     }
+    const bool wall = __builtin_amdgcn_ballot_w64(!done) == 0;
     if (lane == 63) {
       L.xdone[w] = done ? 1 : 0;
       L.xc[w] = cout;
+      L.xall[w] = wall ? 1 : 0;
     }
+    GK_WMARK(5);  // carry walk (counts read, DPP rounds)
     // (one barrier when no chain crosses a wave boundary: the common case)
-    if (__syncthreads_and(done ? 1 : 0)) break;
+    __syncthreads();
+    const int cdone = wg_flags_all(L.xall);
+    GK_WMARK(6);  // carry barrier
+    if (cdone) break;
     if (lane == 0 && w > 0 && !known && L.xdone[w - 1]) {
       known = true;
       cin = L.xc[w - 1];
@@ -2112,7 +2178,9 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
   const uint32_t v = (sm << 16) | so;
   const uint32_t incl = wave_incl_scan_u32(v, lane);
   if (lane == 63) L.wsum[w] = incl;
+  GK_WMARK(7);  // sums + wave scan
   __syncthreads();
+  GK_WMARK(8);  // scan barrier
   uint32_t pre = 0, total = 0;
 #pragma unroll
   for (int k = 0; k < GK_WG_WAVES; ++k) {
@@ -2147,7 +2215,9 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
     }
     if (t == tail_t) gpk[E] = base;
   }
+  GK_WMARK(9);  // wave totals, kept entries and per-gap records stored
   __syncthreads();
+  GK_WMARK(10);  // placement barrier
   GK_BMARK(4);
   if (!sorted) {  // members by gap, in slot order
 #pragma unroll
@@ -2236,7 +2306,9 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
   // +inf padding for the next search, up to pow2_above(newE) - 2
   const int hi = gk_pow2_above(newE) - 1;
   for (int j = newE + t; j < hi; j += GK_WG_T) nv[j] = __longlong_as_double(0x7ff0000000000000LL);
+  GK_WMARK(11);  // values: records read, survivors stored, padding
   __syncthreads();
+  GK_WMARK(12);  // end barrier
   GK_BMARK(6);
   return newE;
 }
@@ -2269,6 +2341,10 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
   if (t == 0) {
     for (int i = 0; i < GK_PROF_NSEC; ++i) gk_big_prof().acc[i] = 0;
     gk_big_prof().t = gk_cycles();
+  }
+  if ((t & 63) == 0 && (t >> 6) < GK_WP_W) {
+    for (int i = 0; i < GK_WP_N; ++i) gk_wave_prof().acc[t >> 6][i] = 0;
+    gk_wave_prof().t[t >> 6] = gk_cycles();
   }
 #endif
   for (;;) {
@@ -2353,7 +2429,9 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
         }
       }
       GK_BMARK(1);
-      const int nE = flush_wg(L, cur, E, xv, cnt, gk_threshold(st, n), t, cur_sorted);
+      GK_WMARK(0);  // between flushes: batch loads, flags
+      const int nE = E <= 2 * GK_WG_T ? flush_wg<2>(L, cur, E, xv, cnt, gk_threshold(st, n), t, cur_sorted)
+                                      : flush_wg<GK_WG_KMAX>(L, cur, E, xv, cnt, gk_threshold(st, n), t, cur_sorted);
       if (!ps_ok) {
         // the flag thread 0 saw at the start of the previous flush (published
         // before this flush's barriers); this flush's reading for the next one
@@ -2390,7 +2468,8 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
           xv[r] = q < cnt ? (q < p ? pb[q] : x[xo + used + (q - p)]) : 0.0;
         }
         n += rem;
-        const int nE = flush_wg(L, cur, E, xv, cnt, gk_threshold(st, n), t, false);
+        const int nE = E <= 2 * GK_WG_T ? flush_wg<2>(L, cur, E, xv, cnt, gk_threshold(st, n), t, false)
+                                        : flush_wg<GK_WG_KMAX>(L, cur, E, xv, cnt, gk_threshold(st, n), t, false);
         if (nE < 0) {
           ok = false;
         } else {
@@ -2432,6 +2511,8 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
 #ifdef GK_PROF
   if (t == 0)
     for (int i = 0; i < GK_PROF_NSEC; ++i) atomicAdd(&gk_prof_acc[i], gk_big_prof().acc[i]);
+  if ((t & 63) == 0 && (t >> 6) < GK_WP_W)
+    for (int i = 0; i < GK_WP_N; ++i) atomicAdd(&gk_wprof_acc[t >> 6][i], gk_wave_prof().acc[t >> 6][i]);
 #endif
 }
 
@@ -5085,6 +5166,13 @@ extern "C" int gk_prof_read(unsigned long long* out) {
 }
 extern "C" int gk_prof_reset() {
   unsigned long long z[GK_PROF_NSEC] = {0};
+  unsigned long long zw[GK_WP_W * GK_WP_N] = {0};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(gk_wprof_acc), zw, sizeof(zw)) != hipSuccess) return -4;
   return hipMemcpyToSymbol(HIP_SYMBOL(gk_prof_acc), z, sizeof(z)) == hipSuccess ? 0 : -4;
+}
+// k_ingest_wg's per-wave marks: [wave][point], GK_WP_W x GK_WP_N
+extern "C" int gk_wprof_read(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(gk_wprof_acc), sizeof(unsigned long long) * GK_WP_W * GK_WP_N) == hipSuccess
+             ? 0 : -4;
 }
 #endif

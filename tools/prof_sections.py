@@ -38,6 +38,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="cfg3", choices=["cfg3", "cfg2", "long", "wg"])
     ap.add_argument("--streams", type=int, default=0)
+    ap.add_argument("--per-wave", action="store_true",
+                    help="wg: per-wave work / barrier-wait split of every stretch of the flush (GK_WMARK)")
     a = ap.parse_args()
     from bench import make_input
     from gkarray_amd import StreamSet
@@ -67,6 +69,19 @@ def main():
         ss.ingest(x, offs, quantiles=[0.5, 0.9, 0.99])
         torch.cuda.synchronize()
     assert lib.gk_prof_read(acc) == 0
+    if a.per_wave:
+        W, N = 8, 16
+        wacc = (ctypes.c_ulonglong * (W * N))()
+        assert lib.gk_wprof_read(wacc) == 0
+        names = ["between flushes (loads)", "setup (zero, g/d loads)", "gap search", "count atomics",
+                 "count barrier", "carry walk", "carry barrier", "sums + wave scan", "scan barrier",
+                 "totals + placement", "placement barrier", "values + pad", "end barrier"]
+        flushes = S * (L // 1001)
+        print("per-wave stretches, cycles per flush (%d flushes): wave0 / min / max over the 8 waves" % flushes)
+        for i, nm in enumerate(names):
+            v = [wacc[w * N + i] / flushes for w in range(W)]
+            print("  %2d %-28s %8.0f %8.0f %8.0f" % (i, nm, v[0], min(v), max(v)))
+        print("  total per flush (wave 0): %.0f" % (sum(wacc[i] for i in range(N)) / flushes))
     tot = sum(acc)
     print("workload %s: %d streams x %d values, total %.3e cycles (sum over waves)" % (a.workload, S, L, tot))
     for i, name in enumerate(SECTIONS):
