@@ -69,6 +69,10 @@ def parse():
                     help="N > 1, cfg2/3/5: strong = split the one batch over the ranks by stream "
                          "(the metric's configuration; the default), weak = every rank its own batch")
     ap.add_argument("--no-weak", action="store_true", help="N > 1 strong: skip the weak line beside it")
+    ap.add_argument("--proxy", type=int, default=0, metavar="N",
+                    help="one process, one GPU: run only rank --proxy-rank's share of the N-way strong split "
+                         "(the single-GPU proxy of an N-GPU run; DESIGN 7)")
+    ap.add_argument("--proxy-rank", type=int, default=0)
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu = the host engine (libgkarray_cpu.so): split / dump checks on CPU only")
     ap.add_argument("--dump", default=None,
@@ -345,7 +349,9 @@ def main():
     if a.eps is None:
         a.eps = 0.001 if a.workload == "cfg5" else 0.01
     qs = [0.5, 0.9, 0.99]
-    split = a.split if a.split != "auto" else ("strong" if world > 1 else "weak")
+    split = a.split if a.split != "auto" else ("strong" if world > 1 or a.proxy > 1 else "weak")
+    if a.proxy > 1 and (world > 1 or not 0 <= a.proxy_rank < a.proxy):
+        sys.exit("bench.py: --proxy runs one rank's share in ONE process (0 <= --proxy-rank < --proxy)")
     if a.workload == "cfg4":
         split = "rows"
 
@@ -416,7 +422,10 @@ def main():
             # the one batch every rank would run alone (same seed on every
             # rank), cut to this rank's streams
             x_full, offs_full = make_batch(5 if a.workload == "cfg5" else a.seed)
-            idx = rank_streams(a.workload, offs_full, world, rank)
+            if a.proxy > 1:
+                idx = rank_streams(a.workload, offs_full, a.proxy, a.proxy_rank)
+            else:
+                idx = rank_streams(a.workload, offs_full, world, rank)
             x, offs = sub_batch(x_full, offs_full, idx)
             del x_full, offs_full
         else:
@@ -469,9 +478,15 @@ def main():
     else:
         lens_txt = ("%d" % L) if a.workload != "cfg5" else "clip(zipf(1.5),1,1e7)"
         if split == "strong":
-            parallelism = ("stream-sharded, strong: the one %d-stream batch split over %d rank(s) by %s "
-                           "(no collective)" % (S, world, "balanced_assignment (longest first)"
-                                                if a.workload == "cfg5" else "stream_range"))
+            if a.proxy > 1:
+                parallelism = ("PROXY of a %d-GPU strong split on 1 GPU: rank %d's share only, by %s (the node "
+                               "rate of an N-rank run is the batch's values / the slowest share's time)"
+                               % (a.proxy, a.proxy_rank, "balanced_assignment (longest first)"
+                                  if a.workload == "cfg5" else "stream_range"))
+            else:
+                parallelism = ("stream-sharded, strong: the one %d-stream batch split over %d rank(s) by %s "
+                               "(no collective)" % (S, world, "balanced_assignment (longest first)"
+                                                    if a.workload == "cfg5" else "stream_range"))
             workload = ("%s: %d streams x %s values (one batch, node), %d on this rank, eps=%g, %s, "
                         "ingest + quantiles(.5,.9,.99)" % (a.workload, S, lens_txt, S_loc, a.eps, dist_name))
         else:

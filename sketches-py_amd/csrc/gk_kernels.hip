@@ -1925,15 +1925,24 @@ struct WgLDS {
 // AND / OR over the workgroup of a per-wave flag (each wave's lane 0 has
 // stored it in f[w] before a plain barrier): two 16-byte LDS reads, where
 // __syncthreads_and / _or are a workgroup reduction with barriers of their own
+static_assert(GK_WG_WAVES % 4 == 0, "per-wave flags are read as int4");
 __device__ __forceinline__ int wg_flags_all(const int32_t* f) {
-  static_assert(GK_WG_WAVES == 8, "two int4 reads");
-  const int4 a = *(const int4*)f, b = *(const int4*)(f + 4);
-  return a.x & a.y & a.z & a.w & b.x & b.y & b.z & b.w;
+  int r = 1;
+#pragma unroll
+  for (int i = 0; i < GK_WG_WAVES; i += 4) {
+    const int4 a = *(const int4*)(f + i);
+    r &= a.x & a.y & a.z & a.w;
+  }
+  return r;
 }
 __device__ __forceinline__ int wg_flags_any(const int32_t* f) {
-  static_assert(GK_WG_WAVES == 8, "two int4 reads");
-  const int4 a = *(const int4*)f, b = *(const int4*)(f + 4);
-  return a.x | a.y | a.z | a.w | b.x | b.y | b.z | b.w;
+  int r = 0;
+#pragma unroll
+  for (int i = 0; i < GK_WG_WAVES; i += 4) {
+    const int4 a = *(const int4*)(f + i);
+    r |= a.x | a.y | a.z | a.w;
+  }
+  return r;
 }
 
 // values q = t + GK_WG_T * r of a batch of cnt in ascending (value, insertion
