@@ -1919,6 +1919,7 @@ struct WgLDS {
   int32_t xdone[GK_WG_WAVES], xc[GK_WG_WAVES];  // the carry walk's wave-boundary states
   alignas(16) int32_t xall[GK_WG_WAVES];  // per wave: every lane's carry-in resolved (the walk's vote)
   alignas(16) int32_t xbig[GK_WG_WAVES];  // per wave: a gap with GK_WG_RANK_MAX members or more
+  alignas(16) int32_t xcrowd[GK_WG_WAVES];  // per wave: a thread with > GK_WG_EMIT_MAX gap survivors
   uint32_t total;
 };
 
@@ -1999,6 +2000,13 @@ __device__ __forceinline__ void wg_sort(WgLDS& L, double (&xv)[GK_WG_VPT], int c
 #ifndef GK_WG_RK_UNROLL
 #define GK_WG_RK_UNROLL 4
 #endif
+// a sorted batch's gap survivors are stored by the thread of their entry
+// (read from the sort area, GK_WG_EMIT_U per trip) unless some thread owns
+// more than GK_WG_EMIT_MAX of them (crowded gaps: the per-gap records path)
+#ifndef GK_WG_EMIT_MAX
+#define GK_WG_EMIT_MAX 16
+#endif
+#define GK_WG_EMIT_U 4
 // KM: table entries per thread, >= ceil(E / GK_WG_T) (2 up to 1024 entries)
 template <int KM>
 __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG_VPT], const int cnt,
@@ -2039,6 +2047,11 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
   const bool nx = has && jend < E;  // the entry after this block (the last entry's removal test)
   const int gnx = nx ? tg[jend] : 0, dnx = nx ? td[jend] : 0;
   const int gp_ = (has && t > 0) ? tg[j0 - 1] : 0, dp_ = (has && t > 0) ? td[j0 - 1] : 0;  // the entry before
+  if (sorted) {  // the batch in order in the sort area, for the entry-side emit (a sort leaves it there too)
+#pragma unroll
+    for (int r = 0; r < GK_WG_VPT; ++r)
+      if (t + GK_WG_T * r < cnt) L.sv[t + GK_WG_T * r] = xv[r];
+  }
   GK_WMARK(1);  // setup: zeroing, the entries' g/d loads issued
   // ---- gap = #entries <= x (gk:93), branch-free over the +inf-padded table
   int xg[GK_WG_VPT];
@@ -2118,6 +2131,9 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
   int ek[KM], eG[KM];  // per entry: absorbed count | KEEP bit, G
 #pragma unroll
   for (int k = 0; k < KM; ++k) ek[k] = eG[k] = 0;
+  const int mEa = (int)gpk[E];            // the tail gap's members
+  const int mE = t == tail_t ? mEa : 0;  // (counted by its thread)
+  uint32_t v = 0, incl = 0;
   for (;;) {
     for (;;) {
       if (known && !done) {
@@ -2149,47 +2165,49 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
       }
       if (__builtin_amdgcn_ballot_w64(nkn) == 0) break;
     }
+    // ---- output offsets: the wave scan of (members << 16 | outputs) of this
+    //      round's results, published with the carry flags: when every
+    //      carry is resolved (the common case, one round) the totals are
+    //      final after this one barrier
+    uint32_t sm = 0, so = 0;
+    int ns = 0;  // gap survivors of this thread's entries
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      if (k < nk) {
+        const int m = em[k], kk = ek[k];
+        sm += (uint32_t)m;
+        so += (uint32_t)(m - (kk & ~GK_KEEP_BIT) + ((kk & GK_KEEP_BIT) ? 1 : 0));
+        ns += m - (kk & ~GK_KEEP_BIT);
+      }
+    }
+    if (t == tail_t) {
+      sm += (uint32_t)mE;
+      so += (uint32_t)((mE + cs - 1) / cs);
+    }
+    v = (sm << 16) | so;
+    incl = wave_incl_scan_u32(v, lane);
     const bool wall = __builtin_amdgcn_ballot_w64(!done) == 0;
+    const bool crowd = __builtin_amdgcn_ballot_w64(ns > GK_WG_EMIT_MAX) != 0;
     if (lane == 63) {
       L.xdone[w] = done ? 1 : 0;
       L.xc[w] = cout;
       L.xall[w] = wall ? 1 : 0;
+      L.xcrowd[w] = crowd ? 1 : 0;
+      L.wsum[w] = incl;
     }
-    GK_WMARK(5);  // carry walk (counts read, DPP rounds)
+    GK_WMARK(5);  // carry walk (counts read, DPP rounds) + sums + wave scan
     // (one barrier when no chain crosses a wave boundary: the common case)
     __syncthreads();
     const int cdone = wg_flags_all(L.xall);
-    GK_WMARK(6);  // carry barrier
+    GK_WMARK(6);  // carry + scan barrier
     if (cdone) break;
     if (lane == 0 && w > 0 && !known && L.xdone[w - 1]) {
       known = true;
       cin = L.xc[w - 1];
     }
-    __syncthreads();  // (xdone / xc are rewritten by the next round)
+    __syncthreads();  // (xdone / xc / wsum are rewritten by the next round)
   }
   GK_BMARK(3);
-
-  // ---- output offsets: one workgroup scan of (members << 16 | outputs) -----
-  uint32_t sm = 0, so = 0;
-#pragma unroll
-  for (int k = 0; k < KM; ++k) {
-    if (k < nk) {
-      const int m = em[k], kk = ek[k];
-      sm += (uint32_t)m;
-      so += (uint32_t)(m - (kk & ~GK_KEEP_BIT) + ((kk & GK_KEEP_BIT) ? 1 : 0));
-    }
-  }
-  if (t == tail_t) {
-    const int mE = (int)gpk[E];
-    sm += (uint32_t)mE;
-    so += (uint32_t)((mE + cs - 1) / cs);
-  }
-  const uint32_t v = (sm << 16) | so;
-  const uint32_t incl = wave_incl_scan_u32(v, lane);
-  if (lane == 63) L.wsum[w] = incl;
-  GK_WMARK(7);  // sums + wave scan
-  __syncthreads();
-  GK_WMARK(8);  // scan barrier
   uint32_t pre = 0, total = 0;
 #pragma unroll
   for (int k = 0; k < GK_WG_WAVES; ++k) {
@@ -2200,6 +2218,89 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
   const int newE = (int)(total & 0xffffu);
   if (newE > GK_WG_CAP - 1) return -1;  // (uniform: total comes from LDS) one slot stays free for the padding
   const int totm = (int)(total >> 16);
+  if (sorted && !wg_flags_any(L.xcrowd)) {
+    // ---- entry-side emit (sorted, no crowded thread): each thread stores its
+    //      entries' gap survivors (sorted positions member base + absorbed ..
+    //      member base + m - 1, gk:93-99) and kept entries, flattened over its
+    //      entries; the tail's values are stored by their own threads
+    //      (gk:85-92).  No per-gap records and no placement barrier.
+    uint32_t base = pre + incl - v;
+    int soff[KM], doff[KM], sb[KM], dl[KM];
+    int st_ = 0;
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      soff[k] = doff[k] = dl[k] = 0;
+      sb[k] = 1 << 30;
+      if (k < nk) {
+        const int j = j0 + k;
+        const int m = em[k], kk = ek[k];
+        const int ka = kk & ~GK_KEEP_BIT;
+        const int ob = (int)(base & 0xffffu);
+        if (kk & GK_KEEP_BIT) {
+          const int pos = ob + m - ka;
+          nv[pos] = tv[j];
+          ng[pos] = eG[k];
+          nd[pos] = ed[k];
+        }
+        sb[k] = st_;
+        soff[k] = (int)(base >> 16) + ka - st_;
+        doff[k] = ob - st_;
+        dl[k] = eG[k] + ed[k] - 1;
+        st_ += m - ka;
+        base += ((uint32_t)m << 16) | (uint32_t)(m - ka + ((kk & GK_KEEP_BIT) ? 1 : 0));
+      }
+    }
+    for (int o0 = 0; o0 < st_; o0 += GK_WG_EMIT_U) {
+      double xs[GK_WG_EMIT_U];
+      int dpos[GK_WG_EMIT_U], dd[GK_WG_EMIT_U];
+#pragma unroll
+      for (int u = 0; u < GK_WG_EMIT_U; ++u) {
+        const int o = o0 + u;
+        int so_ = soff[0], do_ = doff[0], dl_ = dl[0];
+#pragma unroll
+        for (int k = 1; k < KM; ++k)
+          if (o >= sb[k]) {
+            so_ = soff[k];
+            do_ = doff[k];
+            dl_ = dl[k];
+          }
+        xs[u] = L.sv[min(o + so_, GK_WG_PMAX - 1)];
+        dpos[u] = o + do_;
+        dd[u] = dl_;
+      }
+#pragma unroll
+      for (int u = 0; u < GK_WG_EMIT_U; ++u) {
+        if (o0 + u < st_) {
+          nv[dpos[u]] = xs[u];
+          ng[dpos[u]] = 1;
+          nd[dpos[u]] = dd[u];
+        }
+      }
+    }
+    const int mbE = totm - mEa, obE = newE - (mEa + cs - 1) / cs;
+#pragma unroll
+    for (int r = 0; r < GK_WG_VPT; ++r) {
+      const int q = t + GK_WG_T * r;
+      if (q < cnt && xg[r] == E) {
+        const int rk = q - mbE;
+        const int qq = rk / cs;
+        const int rr = rk - qq * cs;
+        if (rr == cs - 1 || rk == mEa - 1) {
+          const int pos = obE + qq;
+          nv[pos] = xv[r];
+          ng[pos] = rr + 1;
+          nd[pos] = 0;
+        }
+      }
+    }
+    const int hi = gk_pow2_above(newE) - 1;
+    for (int j = newE + t; j < hi; j += GK_WG_T) nv[j] = __longlong_as_double(0x7ff0000000000000LL);
+    GK_WMARK(11);
+    __syncthreads();
+    GK_WMARK(12);
+    GK_BMARK(6);
+    return newE;
+  }
   {
     uint32_t base = pre + incl - v;
 #pragma unroll

@@ -45,6 +45,10 @@ def batches(seed):
         seqs[1] = np.round(seqs[1], 1)  # ties
         seqs[2][::97] = 0.0
         seqs[2][::89] = -0.0  # signed zeros
+        # heavy ties: crowded gaps (the per-gap records path of a sorted batch)
+        # and a few values per gap (the entry-side emit)
+        seqs[3] = rng.integers(0, 5, int(lens[3])).astype(np.float64)
+        seqs[4] = rng.integers(0, 3000, int(lens[4])).astype(np.float64)
         if call > 0:  # descending from the second call (k_ingest_wg's first): outgrows 2048 inside it
             seqs[7] = np.linspace(1e6 - call * 1e5, 1.0 - call * 1e5, int(lens[7]))
         out.append(seqs)
