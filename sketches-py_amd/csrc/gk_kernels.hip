@@ -1904,6 +1904,10 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
 #define GK_WG_VPT ((GK_WG_PMAX + GK_WG_T - 1) / GK_WG_T)
 #define GK_WG_KMAX ((GK_WG_CAP + GK_WG_T - 1) / GK_WG_T)  // table entries per thread
 
+// s_waitcnt vmcnt(0) (expcnt / lgkmcnt left at their maxima; gfx9 encoding):
+// every outstanding vector-memory load of the wave has returned
+__device__ __forceinline__ void gk_wait_vmem() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 struct WgLDS {
   double tv[2][GK_WG_CAP];
   int32_t tg[2][GK_WG_CAP];
@@ -2505,7 +2509,6 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
       const int cnt = p + (int)need;
       bool cur_sorted;
       int pf = 0;
-      if (t == 0 && !ps_ok) pf = __hip_atomic_load(ps_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (have_next) {
 #pragma unroll
         for (int r = 0; r < GK_WG_VPT; ++r) xv[r] = xn[r];
@@ -2527,6 +2530,11 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
         }
       }
       n += need;
+      // this batch's loads (if any) complete here, BEFORE the prefetch is
+      // issued: the flush's first use of xv would otherwise wait (vmcnt(0):
+      // the compiler cannot count loads over the three paths above) for the
+      // next batch's loads as well, a full memory latency per flush
+      gk_wait_vmem();
       // prefetch: the next automatic flush's batch (P values: presorted at
       // sb + P, or the call's next P values)
       have_next = used + need + P <= Lx;
@@ -2538,6 +2546,8 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
           xn[r] = q < P ? (next_sorted ? sb[P + q] : x[xo + used + need + q]) : 0.0;
         }
       }
+      // (after the prefetch: read after the flush)
+      if (t == 0 && !ps_ok) pf = __hip_atomic_load(ps_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       GK_BMARK(1);
       GK_WMARK(0);  // between flushes: batch loads, flags
       const int nE = E <= 2 * GK_WG_T ? flush_wg<2>(L, cur, E, xv, cnt, gk_threshold(st, n), t, cur_sorted)
