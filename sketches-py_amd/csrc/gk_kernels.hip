@@ -741,6 +741,9 @@ __device__ __forceinline__ void gk_stat_step(double v, int64_t& n, double& sm, d
 #ifndef GK_SPEC_ROUNDS
 #define GK_SPEC_ROUNDS 16
 #endif
+#ifndef GK_SPEC_GIVEUP
+#define GK_SPEC_GIVEUP 4
+#endif
 
 // inclusive wave64 prefix sum of doubles on DPP (lanes without a source add
 // +0.0); the addition order is the scan's, not a sequential one
@@ -819,6 +822,63 @@ __device__ __forceinline__ double spec_verify(const double (&X)[W + 1], const do
   }
 }
 
+// the gk:52-59 chain of values [k0, k1) of a stream one value at a time:
+// chunks of 64 loaded per lane, then broadcast through LDS (buf) and walked in
+// order by every lane (the chain's latency, ~16 ns per value)
+__device__ __forceinline__ void bcast_walk(const double* __restrict__ x, const int64_t xo, const int64_t k0,
+                                           const int64_t k1, int64_t& n, double& sm, double& av, double& lmn,
+                                           double& lmx, int64_t& imn, int64_t& imx, const int lane, double2* buf) {
+  double q[SL_BCAST_DEPTH];
+#pragma unroll
+  for (int d = 0; d < SL_BCAST_DEPTH; ++d) q[d] = (k0 + 64 * d + lane < k1) ? x[xo + k0 + 64 * d + lane] : 0.0;
+  for (int64_t kc = k0; kc < k1; kc += 64 * SL_BCAST_DEPTH) {
+#pragma unroll
+    for (int d = 0; d < SL_BCAST_DEPTH; ++d) {
+      const int64_t c0 = kc + 64 * d;  // first index of this chunk
+      if (c0 < k1) {
+        const int cn = (int)min((int64_t)64, k1 - c0);
+        const double v = q[d];
+        if (lane < cn) {
+          const int64_t idx = c0 + lane;
+          if (v < lmn) { lmn = v; imn = idx; }
+          if (v > lmx) { lmx = v; imx = idx; }
+        }
+        buf[lane] = make_double2(v, 1.0 / (double)(n + 1 + lane));
+        const int64_t nx = c0 + 64 * SL_BCAST_DEPTH + lane;  // refill: the chunk SL_BCAST_DEPTH ahead
+        q[d] = (nx < k1) ? x[xo + nx] : 0.0;
+        wsync<false>();
+        if (cn == 64) {
+          // keep GK_SL_AHEAD broadcast reads in flight (a ring of registers
+          // refilled as each entry is consumed; sched_barrier pins each
+          // refill before the chain step it hides)
+#ifndef GK_SL_AHEAD
+#define GK_SL_AHEAD 12
+#endif
+          double2 ring[GK_SL_AHEAD];
+#pragma unroll
+          for (int k = 0; k < GK_SL_AHEAD; ++k) ring[k] = buf[k];
+#pragma unroll
+          for (int j = 0; j < 64; ++j) {
+            const double2 e = ring[j % GK_SL_AHEAD];
+            if (j + GK_SL_AHEAD < 64) ring[j % GK_SL_AHEAD] = buf[j + GK_SL_AHEAD];
+            __builtin_amdgcn_sched_barrier(0);
+            sm = sm + e.x;                    // gk:53
+            av = av + (e.x - av) * e.y;       // gk:54
+          }
+        } else {
+          for (int j = 0; j < cn; ++j) {
+            const double2 e = buf[j];
+            sm = sm + e.x;
+            av = av + (e.x - av) * e.y;
+          }
+        }
+        n += cn;  // gk:52
+        wsync<false>();
+      }
+    }
+  }
+}
+
 // one wave walks stream list[w] (the broadcast layout): supersteps of 64 x
 // GK_SPEC_W values by the speculative walk above, the rest one value at a
 // time over LDS broadcasts
@@ -842,6 +902,7 @@ __device__ __forceinline__ void stats_long_bcast(const GKState& st, const double
 #pragma unroll
       for (int t = 0; t < W; ++t) vn[t] = x[xo + lane * W + t];
     }
+    int fails = 0;  // failed supersteps in a row
     for (; kb + SS <= L; kb += SS) {
       double v[W], r[W];
 #pragma unroll
@@ -887,62 +948,25 @@ __device__ __forceinline__ void stats_long_bcast(const GKState& st, const double
       bool ok = true;
       const double av1 = spec_verify<0, W>(XA, v, r, av, lane, ok);
       const double sm1 = ok ? spec_verify<1, W>(XS, v, r, sm, lane, ok) : sm;
-      if (!ok) break;  // this superstep and the rest one at a time (min/max re-seen: same indices, no change)
+      if (!ok) {
+        // this superstep one value at a time (min/max re-seen: same indices,
+        // no change); after GK_SPEC_GIVEUP failed supersteps in a row (the
+        // chains at +-inf or NaN), the rest of the stream too
+        bcast_walk(x, xo, kb, kb + SS, n, sm, av, lmn, lmx, imn, imx, lane, buf);
+        if (++fails == GK_SPEC_GIVEUP) {
+          kb += SS;
+          break;
+        }
+        continue;  // (vn already holds the next superstep's values)
+      }
+      fails = 0;
       av = av1;
       sm = sm1;
       n += SS;  // gk:52
     }
   }
 #endif
-  double q[SL_BCAST_DEPTH];
-#pragma unroll
-  for (int d = 0; d < SL_BCAST_DEPTH; ++d) q[d] = (kb + 64 * d + lane < L) ? x[xo + kb + 64 * d + lane] : 0.0;
-  for (int64_t k0 = kb; k0 < L; k0 += 64 * SL_BCAST_DEPTH) {
-#pragma unroll
-    for (int d = 0; d < SL_BCAST_DEPTH; ++d) {
-      const int64_t c0 = k0 + 64 * d;  // first index of this chunk
-      if (c0 < L) {
-        const int cn = (int)min((int64_t)64, L - c0);
-        const double v = q[d];
-        if (lane < cn) {
-          const int64_t idx = c0 + lane;
-          if (v < lmn) { lmn = v; imn = idx; }
-          if (v > lmx) { lmx = v; imx = idx; }
-        }
-        buf[lane] = make_double2(v, 1.0 / (double)(n + 1 + lane));
-        const int64_t nx = c0 + 64 * SL_BCAST_DEPTH + lane;  // refill: the chunk SL_BCAST_DEPTH ahead
-        q[d] = (nx < L) ? x[xo + nx] : 0.0;
-        wsync<false>();
-        if (cn == 64) {
-          // keep GK_SL_AHEAD broadcast reads in flight (a ring of registers
-          // refilled as each entry is consumed; sched_barrier pins each
-          // refill before the chain step it hides)
-#ifndef GK_SL_AHEAD
-#define GK_SL_AHEAD 12
-#endif
-          double2 ring[GK_SL_AHEAD];
-#pragma unroll
-          for (int k = 0; k < GK_SL_AHEAD; ++k) ring[k] = buf[k];
-#pragma unroll
-          for (int j = 0; j < 64; ++j) {
-            const double2 e = ring[j % GK_SL_AHEAD];
-            if (j + GK_SL_AHEAD < 64) ring[j % GK_SL_AHEAD] = buf[j + GK_SL_AHEAD];
-            __builtin_amdgcn_sched_barrier(0);
-            sm = sm + e.x;                    // gk:53
-            av = av + (e.x - av) * e.y;       // gk:54
-          }
-        } else {
-          for (int j = 0; j < cn; ++j) {
-            const double2 e = buf[j];
-            sm = sm + e.x;
-            av = av + (e.x - av) * e.y;
-          }
-        }
-        n += cn;  // gk:52
-        wsync<false>();
-      }
-    }
-  }
+  bcast_walk(x, xo, kb, L, n, sm, av, lmn, lmx, imn, imx, lane, buf);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const double omn = __shfl_xor(lmn, o, 64), omx = __shfl_xor(lmx, o, 64);
@@ -2436,8 +2460,10 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
                                                        unsigned long long* __restrict__ work,
                                                        const double* __restrict__ psort,
                                                        const int64_t* __restrict__ prio_ws,
-                                                       const int32_t* __restrict__ ps_done, int ps_grid) {
+                                                       const int32_t* __restrict__ ps_done, int ps_grid,
+                                                       int hi_prio) {
   __shared__ WgLDS L;
+  if (hi_prio) __builtin_amdgcn_s_setprio(3);  // (GK_WG_PRIO: the critical chains win the SIMD's issue arbitration)
   __shared__ int64_t item;
   // ps_done: the presort runs beside this launch; a presorted batch is used
   // only once every presort wave has finished (seen by thread 0 with a
@@ -5054,9 +5080,13 @@ hipError_t gk_launch_ingest_wg(const GKState& st, const double* x, const int64_t
   if (st.S <= 0 || !ps.wg_count || !work) return hipSuccess;
   // (at most GK_WG_MAX streams: the count is only known on the device; the
   // spare workgroups find the hand-out exhausted and leave)
+  // raised wave priority (GK_WG_PRIO=0: off): the workgroups' flush chains
+  // are the cfg5 critical path; co-resident waves of the one-wave launch and
+  // the chain walks wait (cfg5 39.4 -> 39.15 ms, profiles/r05/r05x_*)
+  static const int wg_prio = getenv("GK_WG_PRIO") ? atoi(getenv("GK_WG_PRIO")) : 1;
   hipLaunchKernelGGL(k_ingest_wg, dim3(GK_WG_MAX), dim3(GK_WG_T), 0, stream, st, x, offs, long_list, wg_count, lcls,
                      force, ovf_count, ovf_list, work, (const double*)ps.ws, (const int64_t*)ps.list_ws,
-                     (const int32_t*)ps.done, ps.done ? gk_presort_reg_grid(st) : 0);
+                     (const int32_t*)ps.done, ps.done ? gk_presort_reg_grid(st) : 0, wg_prio);
   return hipGetLastError();
 }
 

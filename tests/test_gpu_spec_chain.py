@@ -7,7 +7,8 @@ Parity bar: n/_sum/_avg/_min/_max bit-identical to the C oracle for streams
 past the long-stream limit (16 384 values) with every value distribution the
 parity suite uses plus the ones that make the speculation fail (signed
 magnitudes over e^+-50: several rounds per superstep; infinities and a NaN:
-the round limit hands the stream to the one-at-a-time walk), over two calls
+the round limit hands the superstep, and after four in a row the rest of the
+stream, to the one-at-a-time walk; an isolated burst superstep), over two calls
 (the second starts from a non-trivial pre-call n/_sum/_avg), lengths around
 the superstep size, and with the host walk off (every chain on the device)."""
 import numpy as np
@@ -45,6 +46,15 @@ def batch(seed):
     seqs[25][12] = np.nan
     seqs[36][:] = 1e308  # the _sum overflows to inf part-way
     seqs += [rng.random(int(L)) for L in rng.integers(0, 3000, 24)]  # short streams beside them
+    # one superstep of +-1e20 bursts (each lane's chain absorbs its start
+    # there: every lane fails once, past the round limit) amid lognormal
+    # values: that superstep is walked one at a time, the speculation resumes
+    # after it (round 5; before, the whole rest of the stream was walked)
+    burst = rng.lognormal(0.0, 1.0, 20_000 + (seed - 1) * 333)
+    blk = burst[2048:3072]
+    blk[0::4] = 1e20
+    blk[2::4] = -1e20
+    seqs[-1] = burst
     return seqs
 
 
