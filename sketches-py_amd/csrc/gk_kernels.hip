@@ -1932,10 +1932,16 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
 // every outstanding vector-memory load of the wave has returned
 __device__ __forceinline__ void gk_wait_vmem() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
+// (g, d) pairs: a thread's two entries in one 16-byte read (separate g / d
+// arrays: 0.85 ms more per cfg5 step, profiles/r05/r05B_*; value slots padded
+// against the search probes' bank conflicts -- half the conflict cycles, but
+// slower: 40.4 vs 38.4 ms).  The value buffers are GK_WG_TVN apart, not
+// GK_WG_CAP: a table's slot j and the next table's slot j then fall on
+// different banks (exactly 16 KiB apart: 38.95-39.0 vs 38.4-38.5 ms, r05C)
+#define GK_WG_TVN (GK_WG_CAP + 68)
 struct WgLDS {
-  double tv[2][GK_WG_CAP];
-  int32_t tg[2][GK_WG_CAP];
-  int32_t td[2][GK_WG_CAP];
+  double tv[2][GK_WG_TVN];
+  alignas(16) int2 tgd[2][GK_WG_CAP + 2];
   alignas(16) uint32_t gpk[2][GK_WG_CAP + 4];  // per gap: count, then (member base << 16) | out base; by table parity
   int32_t gk[GK_WG_CAP + 1];    // per entry: absorbed count | KEEP bit
   int32_t gdel[GK_WG_CAP + 1];  // per entry: G, then G + d - 1
@@ -2041,11 +2047,9 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
                         const int T, const int t, bool sorted) {
   const int lane = t & 63, w = t >> 6;
   const double* __restrict__ tv = L.tv[cur];
-  const int32_t* __restrict__ tg = L.tg[cur];
-  const int32_t* __restrict__ td = L.td[cur];
+  const int2* __restrict__ tgd = L.tgd[cur];
   double* __restrict__ nv = L.tv[cur ^ 1];
-  int32_t* __restrict__ ng = L.tg[cur ^ 1];
-  int32_t* __restrict__ nd = L.td[cur ^ 1];
+  int2* __restrict__ ngd = L.tgd[cur ^ 1];
   // per-gap counts / bases: two buffers by table parity; this flush's was
   // zeroed during the previous one (or at stream setup), the other is zeroed
   // now for the next flush (no zeroing pass + barrier before the atomics)
@@ -2066,15 +2070,31 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
   const int cs = T > 1 ? T : 1;
   const int tail_t = E == 0 ? 0 : (E - 1) / K;
   int eg[KM], ed[KM];
+  {
+    int2 gd[KM];
+    if (K % 2 == 0) {  // (j0 even: 16-byte reads of two entries)
 #pragma unroll
-  for (int k = 0; k < KM; ++k) {
-    const bool in = k < nk;
-    eg[k] = in ? tg[j0 + k] : 0;
-    ed[k] = in ? td[j0 + k] : 0;
+      for (int k = 0; k < KM; k += 2) {
+        const int4 a = *(const int4*)&tgd[j0 + k];
+        gd[k] = make_int2(a.x, a.y);
+        if (k + 1 < KM) gd[k + 1] = make_int2(a.z, a.w);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < KM; ++k) gd[k] = tgd[j0 + k];
+    }
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      const bool in = k < nk;
+      eg[k] = in ? gd[k].x : 0;
+      ed[k] = in ? gd[k].y : 0;
+    }
   }
   const bool nx = has && jend < E;  // the entry after this block (the last entry's removal test)
-  const int gnx = nx ? tg[jend] : 0, dnx = nx ? td[jend] : 0;
-  const int gp_ = (has && t > 0) ? tg[j0 - 1] : 0, dp_ = (has && t > 0) ? td[j0 - 1] : 0;  // the entry before
+  const int2 gdn = nx ? tgd[jend] : make_int2(0, 0);
+  const int gnx = gdn.x, dnx = gdn.y;
+  const int2 gdp = (has && t > 0) ? tgd[j0 - 1] : make_int2(0, 0);  // the entry before
+  const int gp_ = gdp.x, dp_ = gdp.y;
   if (sorted) {  // the batch in order in the sort area, for the entry-side emit (a sort leaves it there too)
 #pragma unroll
     for (int r = 0; r < GK_WG_VPT; ++r)
@@ -2267,8 +2287,7 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
         if (kk & GK_KEEP_BIT) {
           const int pos = ob + m - ka;
           nv[pos] = tv[j];
-          ng[pos] = eG[k];
-          nd[pos] = ed[k];
+          ngd[pos] = make_int2(eG[k], ed[k]);
         }
         sb[k] = st_;
         soff[k] = (int)(base >> 16) + ka - st_;
@@ -2300,8 +2319,7 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
       for (int u = 0; u < GK_WG_EMIT_U; ++u) {
         if (o0 + u < st_) {
           nv[dpos[u]] = xs[u];
-          ng[dpos[u]] = 1;
-          nd[dpos[u]] = dd[u];
+          ngd[dpos[u]] = make_int2(1, dd[u]);
         }
       }
     }
@@ -2316,8 +2334,7 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
         if (rr == cs - 1 || rk == mEa - 1) {
           const int pos = obE + qq;
           nv[pos] = xv[r];
-          ng[pos] = rr + 1;
-          nd[pos] = 0;
+          ngd[pos] = make_int2(rr + 1, 0);
         }
       }
     }
@@ -2345,8 +2362,7 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
         if (kk & GK_KEEP_BIT) {
           const int pos = (int)(base & 0xffffu) + m - ka;
           nv[pos] = tv[j];
-          ng[pos] = G;
-          nd[pos] = d;
+          ngd[pos] = make_int2(G, d);
         }
         base += ((uint32_t)m << 16) | (uint32_t)(m - ka + ((kk & GK_KEEP_BIT) ? 1 : 0));
       }
@@ -2425,8 +2441,7 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
         if (rk >= k) {
           const int pos = (int)(pk & 0xffffu) + rk - k;
           nv[pos] = xv[r];
-          ng[pos] = 1;
-          nd[pos] = L.gdel[gap];
+          ngd[pos] = make_int2(1, L.gdel[gap]);
         }
       } else {
         const int m = totm - (int)(pk >> 16);
@@ -2435,8 +2450,7 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
         if (rr == cs - 1 || rk == m - 1) {
           const int pos = (int)(pk & 0xffffu) + qq;
           nv[pos] = xv[r];
-          ng[pos] = rr + 1;
-          nd[pos] = 0;
+          ngd[pos] = make_int2(rr + 1, 0);
         }
       }
     }
@@ -2512,8 +2526,7 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
       for (int j = t; j < E; j += GK_WG_T) {
         const GKRec rc = tab[j];
         L.tv[0][j] = rc.v;
-        L.tg[0][j] = rc.g;
-        L.td[0][j] = rc.d;
+        L.tgd[0][j] = make_int2(rc.g, rc.d);
       }
       const int hi = gk_pow2_above(E) - 1;
       for (int j = E + t; j < hi; j += GK_WG_T) L.tv[0][j] = __longlong_as_double(0x7ff0000000000000LL);
@@ -2642,8 +2655,9 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
     for (int j = t; j < E; j += GK_WG_T) {
       GKRec rc;
       rc.v = L.tv[cur][j];
-      rc.g = L.tg[cur][j];
-      rc.d = L.td[cur][j];
+      const int2 gd = L.tgd[cur][j];
+      rc.g = gd.x;
+      rc.d = gd.y;
       tab[j] = rc;
     }
     if (t == 0) {
