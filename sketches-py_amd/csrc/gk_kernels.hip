@@ -2182,8 +2182,14 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
   const int mEa = (int)gpk[E];            // the tail gap's members
   const int mE = t == tail_t ? mEa : 0;  // (counted by its thread)
   uint32_t v = 0, incl = 0;
+#ifdef GK_PROF
+  int prof_rounds = 0;  // DPP rounds of the carry walk (profiling builds: point 7 counts them)
+#endif
   for (;;) {
     for (;;) {
+#ifdef GK_PROF
+      ++prof_rounds;
+#endif
       if (known && !done) {
         int c = cin;
 #pragma unroll
@@ -2248,6 +2254,10 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
     __syncthreads();
     const int cdone = wg_flags_all(L.xall);
     GK_WMARK(6);  // carry + scan barrier
+#ifdef GK_PROF
+    if ((t & 63) == 0) gk_wave_prof().acc[w][7] += (unsigned long long)prof_rounds * 1000ull;
+    prof_rounds = 0;
+#endif
     if (cdone) break;
     if (lane == 0 && w > 0 && !known && L.xdone[w - 1]) {
       known = true;

@@ -74,14 +74,14 @@ def main():
         wacc = (ctypes.c_ulonglong * (W * N))()
         assert lib.gk_wprof_read(wacc) == 0
         names = ["between flushes (loads)", "setup (zero, g/d loads)", "gap search", "count atomics",
-                 "count barrier", "carry walk", "carry barrier", "sums + wave scan", "scan barrier",
+                 "count barrier", "carry walk", "carry barrier", "carry DPP rounds x1000", "scan barrier",
                  "totals + placement", "placement barrier", "values + pad", "end barrier"]
         flushes = S * (L // 1001)
         print("per-wave stretches, cycles per flush (%d flushes): wave0 / min / max over the 8 waves" % flushes)
         for i, nm in enumerate(names):
             v = [wacc[w * N + i] / flushes for w in range(W)]
             print("  %2d %-28s %8.0f %8.0f %8.0f" % (i, nm, v[0], min(v), max(v)))
-        print("  total per flush (wave 0): %.0f" % (sum(wacc[i] for i in range(N)) / flushes))
+        print("  total per flush (wave 0, cycles): %.0f" % (sum(wacc[i] for i in range(N) if i != 7) / flushes))
     tot = sum(acc)
     print("workload %s: %d streams x %d values, total %.3e cycles (sum over waves)" % (a.workload, S, L, tot))
     for i, name in enumerate(SECTIONS):
