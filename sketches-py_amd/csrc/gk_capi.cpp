@@ -710,14 +710,17 @@ int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s) {
   // unless the small-class launch walks them) and the presort of the long
   // streams' flush batches
   HIP_TRY(gk_launch_stats(h->st, offs, h->d_long_list, h->d_long_count, s));
-  // k_long_prep sorts the list and plans the presort / workgroups, which the
-  // launches on `s` use -- unless the small-class launch carries the stats
-  // role (P <= 128: no presort, no workgroups) and no host chain is picked
-  // from the sorted list: then nothing on `s` reads it before the join, and
-  // it runs on `aux` ahead of k_stats_long (off the ingest's critical path)
-  const bool prep_aux = stats_fused(h) && !(h->hc_min > 0);
-  if (!prep_aux)
-    HIP_TRY(gk_launch_long_prep(h->st, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->ps, s));
+  // k_long_prep sorts the list (longest first) and plans the presort /
+  // workgroups -- unless the small-class launch carries the stats role
+  // (P <= 128: no presort, no workgroups) and no host chain is picked from
+  // the sorted list: then it is not needed at all (k_stats_long reads the
+  // list in k_lengths' order and the pre-call n from k_lengths' snapshot).
+  // k_stats_long must be the first work on `aux` after the fork: queued behind
+  // anything, its waves reach the CUs after the persistent ingest grid and run
+  // ~3x longer beside it (round 5's k_long_prep on aux: cfg4 x 8 shards
+  // 84 -> 118 ms per step, profiles/r05/r05E_*)
+  const bool prep = !(stats_fused(h) && !(h->hc_min > 0));
+  if (prep) HIP_TRY(gk_launch_long_prep(h->st, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->ps, s));
   // the longest chains to host cores: k_hc_prep picks them (k_stats_long
   // skips them) ahead of the fork, so that `aux` holds nothing but
   // k_stats_long and its waves reach the CUs before the ingest grid of this
@@ -745,9 +748,7 @@ int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s) {
   HIP_TRY(hipEventRecord(h->ev_fork, s));
   HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_fork, 0));
   h->forked = true;
-  if (prep_aux)
-    HIP_TRY(gk_launch_long_prep(h->st, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->ps, h->aux));
-  HIP_TRY(gk_launch_stats_long(h->st, x, offs, h->d_long_list, h->d_long_n, h->d_long_count,
+  HIP_TRY(gk_launch_stats_long(h->st, x, offs, h->d_long_list, prep ? h->d_long_n : nullptr, h->d_long_count,
                                hc_on ? h->d_hc_count : nullptr, h->aux));
   h->hc_active = hc_on;  // (stats_join hands the picked chains to the worker)
   HIP_TRY(hipEventRecord(h->ev_join, h->aux));

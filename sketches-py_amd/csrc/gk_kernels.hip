@@ -888,7 +888,7 @@ __device__ __forceinline__ void stats_long_bcast(const GKState& st, const double
   const int64_t s = list[w];
   const int64_t xo = offs[s];
   const int64_t L = offs[s + 1] - xo;
-  int64_t n = list_n[w];
+  int64_t n = list_n ? list_n[w] : st.n0[s];  // (no list_n: k_lengths' pre-call snapshot)
   double sm = st.sum[s], av = st.avg[s];
   double lmn = __longlong_as_double(0x7ff0000000000000LL), lmx = -lmn;
   int64_t imn = INT64_MAX, imx = INT64_MAX;
@@ -1122,7 +1122,8 @@ __global__ __launch_bounds__(64) void k_stats_long(GKState st, const double* __r
   for (int gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
     const int w = gi * 64 + lane;
     const bool act = w < cnt;
-    stats_group_walk(st, x, offs, act ? (int64_t)list[w] : 0, act, act ? list_n[w] : 0, lane, rtile);
+    stats_group_walk(st, x, offs, act ? (int64_t)list[w] : 0, act, act ? (list_n ? list_n[w] : st.n0[list[w]]) : 0,
+                     lane, rtile);
   }
 }
 
