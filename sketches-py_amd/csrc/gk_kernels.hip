@@ -29,6 +29,9 @@
 #include "gk_xor.h"
 
 #define GK_PROF_NSEC 12
+#ifndef GK_PROF_FIRST
+#define GK_PROF_FIRST 1  // k_ingest_small: a wave's first stream's loop tops in section 11
+#endif
 #ifdef GK_PROF
 __device__ unsigned long long gk_prof_acc[GK_PROF_NSEC];
 __device__ __forceinline__ uint32_t gk_cycles() { return (uint32_t)__builtin_amdgcn_s_memtime(); }
@@ -4220,6 +4223,9 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
   };
   int64_t w = grab();
   if (w < count) hv = gk_hdr1_issue<!FS>(st, offs, w, lane);
+#ifdef GK_PROF
+  bool prof_done_any = false;  // a stream of this wave has been written back
+#endif
   for (; w < count;) {
     const int64_t s = w;
     const int64_t wn = grab();
@@ -4306,7 +4312,8 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
       nm1 += (double)(int)nadd;
       const int T = __builtin_amdgcn_readfirstlane((int)(st.two_eps * nm1));
       const CsDiv cd = make_csdiv(T);
-      GK_MARK(L, 8);
+      // (profiling builds: the loop top of a wave's FIRST stream counts apart, in 11)
+      GK_MARK(L, (GK_PROF_FIRST && !prof_done_any) ? 11 : 8);
       int nE;
       if constexpr (SMALL_CAP > 128)
         nE = E <= 127 ? flush_small<VPL, 2>(L, E, xv, cnt, T, cd, lane, prefetch)
@@ -4387,6 +4394,9 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
     write_back();
     wsync<false>();
     GK_MARK(L, 9);
+#ifdef GK_PROF
+    prof_done_any = true;
+#endif
   }
 #ifdef GK_PROF
   if (lane == 0)

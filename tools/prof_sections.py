@@ -23,7 +23,7 @@ import torch  # noqa: E402
 SECTIONS = ["stream setup (header, table load)", "gap search", "counts (zero, atomics, max gap)",
             "entries + carry + scan", "keeps + per-gap info", "rank loop + emit", "bitonic sort + emit",
             "pad + end of flush", "between flushes (T, next flush setup)", "leftover, quantiles, write-back",
-            "next flush's values (prefetch wait)", "-"]
+            "next flush's values (prefetch wait)", "between flushes, a wave's first stream"]
 
 SECTIONS_WG = ["stream setup + loop top", "batch load + next-batch prefetch", "gap search + counts",
                "carry walk", "scan + per-gap bases + keeps", "member stores (unsorted)",
