@@ -2566,6 +2566,11 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
 #pragma unroll
         for (int r = 0; r < GK_WG_VPT; ++r) xv[r] = xn[r];
         cur_sorted = next_sorted;
+#ifdef GK_PROF
+        // (profiling builds: point 13 = the wait for the prefetched batch)
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        GK_WMARK(13);
+#endif
       } else if (sb && ps_ok && (flushed || !ps_done)) {
         // (beside the presort, batch 0 is never sorted: k_presort_reg)
         cur_sorted = true;

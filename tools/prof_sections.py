@@ -36,27 +36,31 @@ SECTIONS_BIG = ["stream setup (header, table load)", "gap search", "counts (zero
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", default="cfg3", choices=["cfg3", "cfg2", "long", "wg"])
+    ap.add_argument("--workload", default="cfg3", choices=["cfg3", "cfg2", "long", "wg", "cfg5"])
     ap.add_argument("--streams", type=int, default=0)
     ap.add_argument("--per-wave", action="store_true",
                     help="wg: per-wave work / barrier-wait split of every stretch of the flush (GK_WMARK)")
     a = ap.parse_args()
-    from bench import make_input
+    from bench import make_input, make_zipf_input
     from gkarray_amd import StreamSet
     S, L, dist_name = {"cfg3": (1_000_000, 1000, "pareto"), "cfg2": (100_000, 10_000, "lognormal"),
-                       "long": (64, 1_000_000, "lognormal"), "wg": (64, 1_000_000, "lognormal")}[a.workload]
+                       "long": (64, 1_000_000, "lognormal"), "wg": (64, 1_000_000, "lognormal"),
+                       "cfg5": (100_000, 0, "zipf")}[a.workload]
     S = a.streams or S
     dev = torch.device("cuda", 0)
-    x, offs = make_input(S, L, 3, dev, dist_name)
+    if a.workload == "cfg5":  # the bench's cfg5 batch: every k_ingest_wg stream beside everything else
+        x, offs = make_zipf_input(S, 5, dev)
+    else:
+        x, offs = make_input(S, L, 3, dev, dist_name)
     # "long": eps=0.001 streams of 1M values in the 2048 class (k_ingest<2048>,
     # sections of flush_wave: SECTIONS_BIG)
     # "wg": the same streams through k_ingest_wg (GK_WG=1; GK_WG_PRESORT from
     # the environment), sections of flush_wg: SECTIONS_WG
-    eps = 0.001 if a.workload in ("long", "wg") else 0.01
+    eps = 0.001 if a.workload in ("long", "wg", "cfg5") else 0.01
     global SECTIONS
     if a.workload == "long":
         SECTIONS = SECTIONS_BIG
-    if a.workload == "wg":
+    if a.workload in ("wg", "cfg5"):
         os.environ["GK_WG"] = "1"
         SECTIONS = SECTIONS_WG
     ss = StreamSet(S, eps, device=dev)
@@ -75,8 +79,13 @@ def main():
         assert lib.gk_wprof_read(wacc) == 0
         names = ["between flushes (loads)", "setup (zero, g/d loads)", "gap search", "count atomics",
                  "count barrier", "carry walk", "carry barrier", "carry DPP rounds x1000", "scan barrier",
-                 "totals + placement", "placement barrier", "values + pad", "end barrier"]
+                 "totals + placement", "placement barrier", "values + pad", "end barrier",
+                 "loop top up to the batch copy (incl. its wait)"]
         flushes = S * (L // 1001)
+        if a.workload == "cfg5":  # the workgroup streams: >= 256 flushes, the 64 longest (GK_WG_MAX)
+            lens = sorted(((offs[1:] - offs[:-1]).cpu().tolist()), reverse=True)
+            wl = [n for n in lens if n // 1001 >= 256][:64]
+            flushes = sum(n // 1001 for n in wl)
         print("per-wave stretches, cycles per flush (%d flushes): wave0 / min / max over the 8 waves" % flushes)
         for i, nm in enumerate(names):
             v = [wacc[w * N + i] / flushes for w in range(W)]
