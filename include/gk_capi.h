@@ -133,9 +133,11 @@ int gk_stats(gk_set* set, int64_t* n, double* mn, double* mx, double* sum,
 
 /* GKArray.merge(other) (gk:111-154), stream by stream, as the left fold
  * dst.merge(srcs[0]); dst.merge(srcs[1]); ...  Like the reference it mutates
- * each source (flushes its pending values, gk:126, 137).  Returns
- * GK_E_EPS_MISMATCH if any eps differs (gk:118-119) or GK_E_ARG if the
- * stream counts differ. */
+ * each source (flushes its pending values, gk:126, 137).  A source may be dst
+ * itself (dst.merge(dst): dst is flushed, then merged with a snapshot of its
+ * flushed state, as gk:137-154 do) and may repeat (flushed again at each of
+ * its merges).  Returns GK_E_EPS_MISMATCH if any eps differs (gk:118-119) or
+ * GK_E_ARG if the stream counts differ. */
 int gk_merge(gk_set* dst, gk_set* const* srcs, int nsrcs, void* stream);
 
 /* GKArray.merge_compress(entries) with an explicit entry list (gk:63-109,
