@@ -98,6 +98,24 @@ def test_strong_split_cfg5_balanced_cpu(tmp_path):
     assert all(len(p["idx"]) > 0 for p in parts)
 
 
+def test_proxy_ranks_cover_the_split_cpu(tmp_path):
+    """`bench.py --proxy N --proxy-rank R` (one process: rank R's share of the
+    N-way strong split, the single-GPU proxies of DESIGN 7) runs exactly the
+    streams rank R of an N-rank run would, with the same quantiles."""
+    S, N = 1000, 3
+    args = ["--workload", "cfg5", "--streams", str(S), "--values", "20000", "--device", "cpu"]
+    run_bench(args, 1, str(tmp_path / "one"))
+    q1 = np.load(str(tmp_path / "one") + ".rank0.npz")["q"]
+    seen = []
+    for r in range(N):
+        line = run_bench(args + ["--proxy", str(N), "--proxy-rank", str(r)], 1, str(tmp_path / ("p%d" % r)))
+        assert line["n_gpus"] == 1 and "PROXY" in line["config"]["parallelism"]
+        d = np.load(str(tmp_path / ("p%d" % r)) + ".rank0.npz")
+        assert np.array_equal(d["q"].view(np.int64), q1[d["idx"]].view(np.int64))
+        seen.append(d["idx"])
+    assert np.array_equal(np.sort(np.concatenate(seen)), np.arange(S))
+
+
 @pytest.mark.gpu
 def test_strong_split_cfg3_rehearsal_on_device(tmp_path):
     import torch
