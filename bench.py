@@ -26,6 +26,7 @@ under "weak" (``--split weak`` makes it the headline; ``--no-weak`` skips it).
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -360,12 +361,39 @@ def main():
             return make_zipf_input(S, seed, dev, cap=a.values or 10_000_000)
         return make_input(S, L, seed, dev, dist_name)
 
+    # Untimed warm-up: the W steps asked for, then more until the warm-up has
+    # lasted min_warm seconds.  The shader clock ramps over tens of ms of
+    # load (measured 2.00 GHz after 4 cfg3 steps at 125k streams, 2.38 GHz
+    # after 100; 1M streams: 2.00 GHz after 1 step, 2.38 after 40 --
+    # profiles/r05/r05Z_clock_ramp.txt): without it a short run times the
+    # ramp, not the engine.  The extra count is agreed over ranks (the same
+    # number of steps everywhere: cfg4's steps hold collectives).
+    min_warm = float(os.environ.get("GK_BENCH_MIN_WARM_S", "0.3" if on_gpu else "0"))
+    warm_info = {"steps": 0, "seconds": 0.0}
+
     def timed(step, timed_sets):
-        """W untimed steps, then K steps bracketed by barrier + device sync;
+        """W (+ extra, see min_warm) untimed steps, then K steps bracketed by barrier + device sync;
         (max-over-ranks seconds, launch ms summed over sets, stats ms, launches, last result)."""
+        gsync()
+        tw = time.perf_counter()
+        nw = 0
         for _ in range(a.warmup):
             step()
+            nw += 1
+        if min_warm > 0:
+            if nw == 0:
+                step()
+                nw = 1
+            gsync()
+            el = time.perf_counter() - tw
+            extra = 0 if el >= min_warm else min(5000, int(math.ceil((min_warm - el) / (el / nw))))
+            import torch.distributed as _dd
+            extra = int(allreduce(float(extra), _dd.ReduceOp.MAX))
+            for _ in range(extra):
+                step()
+            nw += extra
         gsync()
+        warm_info["steps"], warm_info["seconds"] = nw, time.perf_counter() - tw
         for t_ss in timed_sets:
             t_ss.timing(True)
             t_ss.read_timing()
@@ -500,6 +528,9 @@ def main():
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
+        "warmup_run": {"steps": warm_info["steps"], "seconds": round(warm_info["seconds"], 4),
+                       "min_seconds": min_warm, "why": "untimed; the GPU clock ramps over tens of ms of load "
+                       "(profiles/r05/r05Z_clock_ramp.txt)"},
         "ms_per_step": ms_step,
         "higher_is_better": True,
         "scaling": "weak" if split == "weak" else "strong",
