@@ -4182,6 +4182,15 @@ __device__ __forceinline__ void fused_stats_role(const GKState& st, const double
 // during it, so the header prefetch skips them and fused quantiles use markers.
 // Class 0 over every stream only (promoted streams are skipped: their class's
 // launch runs them).
+#ifdef GK_TIMELINE
+// timeline builds only (tools/launch_timeline.py): s_memrealtime (100 MHz,
+// chip-wide) per wave (start, stats role done, end) and per stream (start, end)
+#define GK_TL_MAXS (1 << 20)
+#define GK_TL_MAXW 16384
+__device__ unsigned long long gk_tl_wave[5 * GK_TL_MAXW];
+__device__ unsigned long long gk_tl_sbeg[GK_TL_MAXS];
+__device__ unsigned long long gk_tl_send[GK_TL_MAXS];
+#endif
 template <int VPL, bool FS>
 __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st, const double* __restrict__ x,
                                                      const int64_t* __restrict__ offs, int64_t count, int force,
@@ -4211,7 +4220,16 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
 #endif
   const int nparts = (int)min((unsigned)GK_WORK_PARTS, gridDim.x);  // every part has a wave
   const int part = (int)(blockIdx.x % (unsigned)nparts);
+#ifdef GK_TIMELINE
+  if (lane == 0 && blockIdx.x < GK_TL_MAXW) {
+    gk_tl_wave[5 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    gk_tl_wave[5 * blockIdx.x + 3] = __builtin_amdgcn_s_memtime();
+  }
+#endif
   if (FS && (int)blockIdx.x < nstat) fused_stats_role(st, x, offs, work, part, nparts, count, fs_pace, fs_lag, lane);
+#ifdef GK_TIMELINE
+  if (lane == 0 && blockIdx.x < GK_TL_MAXW) gk_tl_wave[5 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
   const int64_t pbeg = count * part / nparts, pend = count * (part + 1) / nparts;
   // the query's q values, the same for every stream: lane l holds q l
   const double qpre = (qs && lane < nq) ? qs[lane] : 0.0;
@@ -4247,6 +4265,9 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
     if (wn < count) hv = gk_hdr1_issue<!FS>(st, offs, wn, lane);
     w = wn;
     if (scls != 0) continue;  // promoted: handled by its class launch
+#ifdef GK_TIMELINE
+    if (lane == 0 && s < GK_TL_MAXS) gk_tl_sbeg[s] = __builtin_amdgcn_s_memrealtime();
+#endif
     const int64_t Lx = xe - xo;
     // force 1: flush only if values are pending (size/quantile, gk:45, 166, 197)
     // force 2: unconditional merge_compress() (merge, gk:122, 126, 137)
@@ -4399,6 +4420,9 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
     write_back();
     wsync<false>();
     GK_MARK(L, 9);
+#ifdef GK_TIMELINE
+    if (lane == 0 && s < GK_TL_MAXS) gk_tl_send[s] = __builtin_amdgcn_s_memrealtime();
+#endif
 #ifdef GK_PROF
     prof_done_any = true;
 #endif
@@ -4406,6 +4430,12 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
 #ifdef GK_PROF
   if (lane == 0)
     for (int i = 0; i < GK_PROF_NSEC; ++i) atomicAdd(&gk_prof_acc[i], L.prof[i]);
+#endif
+#ifdef GK_TIMELINE
+  if (lane == 0 && blockIdx.x < GK_TL_MAXW) {
+    gk_tl_wave[5 * blockIdx.x + 2] = __builtin_amdgcn_s_memrealtime();
+    gk_tl_wave[5 * blockIdx.x + 4] = __builtin_amdgcn_s_memtime();
+  }
 #endif
 }
 
@@ -5349,6 +5379,15 @@ hipError_t gk_launch_promote(const GKState& st, const int32_t* list, int64_t cou
   return hipGetLastError();
 }
 
+#ifdef GK_TIMELINE
+// timeline builds only (tools/launch_timeline.py; not part of include/gk_capi.h)
+extern "C" int gk_tl_read(unsigned long long* wave, unsigned long long* sbeg, unsigned long long* send) {
+  if (hipDeviceSynchronize() != hipSuccess) return -4;
+  if (hipMemcpyFromSymbol(wave, HIP_SYMBOL(gk_tl_wave), sizeof(unsigned long long) * 5 * GK_TL_MAXW) != hipSuccess) return -4;
+  if (hipMemcpyFromSymbol(sbeg, HIP_SYMBOL(gk_tl_sbeg), sizeof(unsigned long long) * GK_TL_MAXS) != hipSuccess) return -4;
+  return hipMemcpyFromSymbol(send, HIP_SYMBOL(gk_tl_send), sizeof(unsigned long long) * GK_TL_MAXS) == hipSuccess ? 0 : -4;
+}
+#endif
 #ifdef GK_PROF
 // profiling builds only (not part of include/gk_capi.h)
 extern "C" int gk_prof_read(unsigned long long* out) {
