@@ -5031,9 +5031,12 @@ static hipError_t launch_ingest_t(const GKState& st, const double* x, const int6
   int64_t grid;
   if (CAP > 0) {
     // one resident wave per slot; streams are handed out through `work`
-    int occ = 0;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_ingest<CAP, VPL>, 64, 0);
-    if (occ <= 0) occ = 1;
+    // (the occupancy query is a host API call of several us: once per kernel)
+    static int occ = 0;
+    if (occ <= 0) {
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_ingest<CAP, VPL>, 64, 0);
+      if (occ <= 0) occ = 1;
+    }
     grid = (int64_t)num_cu() * occ;
   } else {
     grid = ws_blocks;
@@ -5074,9 +5077,11 @@ static hipError_t launch_ingest_small(const GKState& st, const double* x, const 
                                       hipStream_t stream) {
   if (count <= 0) return hipSuccess;
   if (!work) return hipErrorInvalidValue;
-  int occ = 0;
-  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_ingest_small<VPL, false>, 64, 0);
-  if (occ <= 0) occ = 1;
+  static int occ = 0;  // (queried once: a host API call of several us)
+  if (occ <= 0) {
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_ingest_small<VPL, false>, 64, 0);
+    if (occ <= 0) occ = 1;
+  }
   // one resident wave per slot; streams are handed out through `work`
   int64_t grid = (int64_t)num_cu() * occ;
   if (grid > count) grid = count;

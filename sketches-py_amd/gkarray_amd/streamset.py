@@ -76,7 +76,11 @@ class StreamSet:
         return self.device.type == "cpu"
 
     def _ctx(self):
-        return contextlib.nullcontext() if self.device.type == "cpu" else torch.cuda.device(self.device)
+        # (no device switch when the set's device is already current: the
+        # context manager's get/set round trip is host time on every call)
+        if self.device.type == "cpu" or torch.cuda.current_device() == self.device.index:
+            return contextlib.nullcontext()
+        return torch.cuda.device(self.device)
 
     def _check(self, rc):
         return L.check(rc, self._lib)
