@@ -384,14 +384,17 @@ def main():
             if nw == 0:
                 step()
                 nw = 1
-            gsync()
-            el = time.perf_counter() - tw
-            extra = 0 if el >= min_warm else min(5000, int(math.ceil((min_warm - el) / (el / nw))))
             import torch.distributed as _dd
-            extra = int(allreduce(float(extra), _dd.ReduceOp.MAX))
-            for _ in range(extra):
-                step()
-            nw += extra
+            for _ in range(4):  # (steps get faster as the clock ramps: re-estimate)
+                gsync()
+                el = time.perf_counter() - tw
+                extra = 0 if el >= min_warm else min(5000, int(math.ceil((min_warm - el) / (el / nw))))
+                extra = int(allreduce(float(extra), _dd.ReduceOp.MAX))
+                if extra == 0:
+                    break
+                for _ in range(extra):
+                    step()
+                nw += extra
         gsync()
         warm_info["steps"], warm_info["seconds"] = nw, time.perf_counter() - tw
         for t_ss in timed_sets:
