@@ -332,8 +332,16 @@ __device__ __forceinline__ GKRec* gk_table_ptr_cs(const GKState& st, int64_t s, 
 // launch's stats role while its ingest waves rewrite st.n): one stream per
 // thread, no LDS (~6 us per 10^6 streams; as part of the former k_stats, whose 35 KiB
 // chain tile holds it to 4 blocks per CU, it took 28 us).
+#ifdef GK_TIMELINE
+// timeline builds only: s_memrealtime when the call's first kernel starts
+// (k_lengths) and when its join answers (k_query_list)
+__device__ unsigned long long gk_tl_call[2];
+#endif
 __global__ __launch_bounds__(256) void k_lengths(GKState st, const int64_t* __restrict__ offs,
                                                  int32_t* __restrict__ long_list, int32_t* __restrict__ long_count) {
+#ifdef GK_TIMELINE
+  if (blockIdx.x == 0 && threadIdx.x == 0) gk_tl_call[0] = __builtin_amdgcn_s_memrealtime();
+#endif
   const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (s >= st.S) return;
   st.n0[s] = st.n[s];
@@ -1646,6 +1654,9 @@ __global__ __launch_bounds__(256) void k_query_list(GKState st, const int32_t* _
                                                     const double* __restrict__ qs, int nq, int qmode,
                                                     double* __restrict__ qout, int qfix) {
   const int lane = threadIdx.x & 63;
+#ifdef GK_TIMELINE
+  if (blockIdx.x == 0 && threadIdx.x == 0) gk_tl_call[1] = __builtin_amdgcn_s_memrealtime();
+#endif
   if (qfix) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i < st.S * (int64_t)nq) {
@@ -2479,6 +2490,11 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
   return newE;
 }
 
+#ifdef GK_TIMELINE
+// timeline builds only: per workgroup of k_ingest_wg, s_memrealtime and
+// s_memtime at its start and end, and its flushes (tools/launch_timeline.py)
+__device__ unsigned long long gk_tl_wg[5 * GK_WG_MAX];
+#endif
 __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double* __restrict__ x,
                                                        const int64_t* __restrict__ offs,
                                                        const int32_t* __restrict__ prio,
@@ -2492,6 +2508,12 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
                                                        int hi_prio) {
   __shared__ WgLDS L;
   if (hi_prio) __builtin_amdgcn_s_setprio(3);  // (GK_WG_PRIO: the critical chains win the SIMD's issue arbitration)
+#ifdef GK_TIMELINE
+  if (threadIdx.x == 0 && blockIdx.x < GK_WG_MAX) {
+    gk_tl_wg[5 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    gk_tl_wg[5 * blockIdx.x + 1] = __builtin_amdgcn_s_memtime();
+  }
+#endif
   __shared__ int64_t item;
   // ps_done: the presort runs beside this launch; a presorted batch is used
   // only once every presort wave has finished (seen by thread 0 with a
@@ -2692,6 +2714,13 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
     for (int i = 0; i < GK_PROF_NSEC; ++i) atomicAdd(&gk_prof_acc[i], gk_big_prof().acc[i]);
   if ((t & 63) == 0 && (t >> 6) < GK_WP_W)
     for (int i = 0; i < GK_WP_N; ++i) atomicAdd(&gk_wprof_acc[t >> 6][i], gk_wave_prof().acc[t >> 6][i]);
+#endif
+#ifdef GK_TIMELINE
+  if (t == 0 && blockIdx.x < GK_WG_MAX) {
+    gk_tl_wg[5 * blockIdx.x + 2] = __builtin_amdgcn_s_memrealtime();
+    gk_tl_wg[5 * blockIdx.x + 3] = __builtin_amdgcn_s_memtime();
+    gk_tl_wg[5 * blockIdx.x + 4] = (unsigned long long)fk;
+  }
 #endif
 }
 
@@ -5391,6 +5420,14 @@ extern "C" int gk_tl_read(unsigned long long* wave, unsigned long long* sbeg, un
   if (hipMemcpyFromSymbol(wave, HIP_SYMBOL(gk_tl_wave), sizeof(unsigned long long) * 5 * GK_TL_MAXW) != hipSuccess) return -4;
   if (hipMemcpyFromSymbol(sbeg, HIP_SYMBOL(gk_tl_sbeg), sizeof(unsigned long long) * GK_TL_MAXS) != hipSuccess) return -4;
   return hipMemcpyFromSymbol(send, HIP_SYMBOL(gk_tl_send), sizeof(unsigned long long) * GK_TL_MAXS) == hipSuccess ? 0 : -4;
+}
+extern "C" int gk_tl_call_read(unsigned long long* c) {
+  if (hipDeviceSynchronize() != hipSuccess) return -4;
+  return hipMemcpyFromSymbol(c, HIP_SYMBOL(gk_tl_call), sizeof(unsigned long long) * 2) == hipSuccess ? 0 : -4;
+}
+extern "C" int gk_tl_wg_read(unsigned long long* wg) {
+  if (hipDeviceSynchronize() != hipSuccess) return -4;
+  return hipMemcpyFromSymbol(wg, HIP_SYMBOL(gk_tl_wg), sizeof(unsigned long long) * 5 * GK_WG_MAX) == hipSuccess ? 0 : -4;
 }
 #endif
 #ifdef GK_PROF

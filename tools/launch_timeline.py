@@ -33,12 +33,59 @@ def pct(a, qs=(0, 1, 10, 50, 90, 99, 100)):
     return " ".join("p%d=%.1f" % (q, np.percentile(a, q)) for q in qs)
 
 
+def wg_clock(arg, lib, dev):
+    """k_ingest_wg's workgroups: wall time, flushes, us per flush and shader
+    clock per workgroup.  "wg:cfg5": the bench's cfg5 batch (everything
+    beside the workgroups); "wg:S": S lognormal streams of 10^7 values alone."""
+    from bench import make_zipf_input
+    from gkarray_amd import StreamSet
+    what = arg.split(":")[1] if ":" in arg else "cfg5"
+    if what == "cfg5":
+        x, offs = make_zipf_input(100_000, 5, dev)
+    else:
+        S, L = int(what), 10_000_000
+        g = torch.Generator(device=dev).manual_seed(5)
+        x = torch.exp(torch.randn(S * L, device=dev, dtype=torch.float64, generator=g))
+        offs = torch.arange(S + 1, device=dev, dtype=torch.int64) * L
+    ss = StreamSet(offs.numel() - 1, 0.001, device=dev)
+    for _ in range(int(os.environ.get("TL_WARM", "4"))):
+        ss.reset()
+        ss.ingest(x, offs, quantiles=[0.5, 0.9, 0.99])
+    torch.cuda.synchronize()
+    wg = np.zeros(5 * 64, dtype=np.uint64)
+    assert lib.gk_tl_wg_read(wg.ctypes.data_as(ctypes.c_void_p)) == 0
+    w = wg.reshape(-1, 5).astype(np.int64)
+    w = w[(w[:, 0] > 0) & (w[:, 4] > 0)]
+    dur = (w[:, 2] - w[:, 0]) / 100.0
+    clk = (w[:, 3] - w[:, 1]) / np.maximum(w[:, 2] - w[:, 0], 1) * 100.0
+    fl = w[:, 4]
+    print("%s (%s warm-up steps): %d workgroups with flushes" % (arg, os.environ.get("TL_WARM", "4"), len(w)))
+    order = np.argsort(-fl)
+    cl = np.zeros(2, dtype=np.uint64)
+    assert lib.gk_tl_call_read(cl.ctypes.data_as(ctypes.c_void_p)) == 0
+    t0 = int(cl[0])  # the call's first kernel (k_lengths)
+    st_us, en_us = (w[:, 0] - t0) / 100.0, (w[:, 2] - t0) / 100.0
+    print("  the call: k_lengths start -> k_query_list (the join) %.0f us; first workgroup start %.0f us"
+          % ((int(cl[1]) - t0) / 100.0, st_us.min()))
+    print("  flushes   start us   end us   wall us   us/flush   clock MHz   (the 12 longest chains; times from the call's first kernel)")
+    for i in order[:12]:
+        print("  %7d %9.0f %8.0f %9.0f %10.3f %11.0f" % (fl[i], st_us[i], en_us[i], dur[i], dur[i] / fl[i], clk[i]))
+    print("  workgroup start us:", pct(st_us))
+    print("  workgroup end us:  ", pct(en_us))
+    print("  clock MHz over all workgroups:", pct(clk))
+    del ss, x, offs
+    torch.cuda.empty_cache()
+
+
 def main():
     from bench import make_input
     from gkarray_amd import StreamSet
     dev = torch.device("cuda", 0)
     lib = ctypes.CDLL(os.environ["GK_LIB_PATH"])
     for arg in sys.argv[1:] or ["125000", "1000000"]:
+        if arg.startswith("wg"):
+            wg_clock(arg, lib, dev)
+            continue
         f = arg.split(":")
         S, L = int(f[0]), int(f[1]) if len(f) > 1 else 1000
         x, offs = make_input(S, L, 3, dev, "pareto")
