@@ -168,6 +168,8 @@ struct gk_set {
   bool presort_active = false;   // a presort of this call not yet joined on the caller's stream
   hipEvent_t ev_presort = nullptr;
   hipEvent_t ev_wg = nullptr;  // k_ingest_wg (on aux2, after the presort) done
+  hipEvent_t ev_go = nullptr;  // the call's counters zeroed: k_ingest_wg may be launched (GK_WG_EARLY)
+  bool wg_early = false;       // this call's k_ingest_wg was launched by stats_fork, ahead of the chain walks
   bool wg_trace = false;       // GK_WG_TRACE=1 at creation: its stream count per completed call on stderr (tests)
   std::vector<hipStream_t> hc_streams;
   std::vector<double*> hc_buf;
@@ -687,6 +689,8 @@ void hc_shutdown(gk_set* h) {
 // waits for the aux work, and chains the host would have walked are walked on
 // the device (k_hc_fallback with the fail word set).
 void stats_abort(gk_set* h, hipStream_t s) {
+  if (h->wg_early) (void)hipStreamWaitEvent(s, h->ev_wg, 0);  // (launched by stats_fork: joined here too)
+  h->wg_early = false;
   if (h->forked) (void)hipStreamWaitEvent(s, h->ev_join, 0);
   if (h->presort_active) (void)hipStreamWaitEvent(s, h->ev_presort, 0);
   h->presort_active = false;
@@ -701,9 +705,20 @@ void stats_abort(gk_set* h, hipStream_t s) {
   h->hc_active = false;
 }
 
-int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s) {
+int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s, int force) {
   hipEvent_t t0 = h->timing ? timing_event(h->tev_stats, h->n_stats) : nullptr;
   if (t0) HIP_TRY(hipEventRecord(t0, s));
+  // k_ingest_wg ahead of everything else of the call (GK_WG_EARLY, default
+  // 1): launched behind the call's counter reset only, its workgroups take
+  // their CUs (128 KiB of LDS and 8 waves each) while the chip is still
+  // empty and wait on the device for k_long_prep's word; queued behind it,
+  // they found the CUs held by the chain walks and the presort and started
+  // 3.1-4.2 ms into a 38.9 ms cfg5 call (profiles/r05/r05AF3_*).  Launched
+  // only after k_long_prep is enqueued, so that the word is always written.
+  static const int early_env = getenv("GK_WG_EARLY") ? atoi(getenv("GK_WG_EARLY")) : 1;
+  h->wg_early = false;
+  const bool early = early_env && x && h->ps.done && h->ps.wg_count && h->aux2 && h->ps.list_ws;
+  if (early) HIP_TRY(hipEventRecord(h->ev_go, s));
   // the long-stream list (k_lengths) + k_long_prep, then the fork
   // (k_stats_long needs only the sorted list and the pre-call n: the longest
   // chains start at once), then on `s` the short streams' chains (k_stats,
@@ -720,7 +735,18 @@ int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s) {
   // ~3x longer beside it (round 5's k_long_prep on aux: cfg4 x 8 shards
   // 84 -> 118 ms per step, profiles/r05/r05E_*)
   const bool prep = !(stats_fused(h) && !(h->hc_min > 0));
-  if (prep) HIP_TRY(gk_launch_long_prep(h->st, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->ps, s));
+  if (prep)
+    HIP_TRY(gk_launch_long_prep(h->st, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->ps, s,
+                                early ? h->d_ctr + GK_CTR_WGGO : nullptr));
+  if (early && prep) {
+    unsigned long long* wwork = work_counter(h, false);
+    if (!wwork) return fail(GK_E_HIP, "no hand-out counter left for k_ingest_wg");
+    HIP_TRY(hipStreamWaitEvent(h->aux2, h->ev_go, 0));
+    HIP_TRY(gk_launch_ingest_wg(h->st, x, offs, h->d_long_list, h->ps.wg_count, 0, force, ovf_count(h, 0),
+                                ovf_list(h, 0), wwork, h->ps, h->aux2, h->d_ctr + GK_CTR_WGGO));
+    HIP_TRY(hipEventRecord(h->ev_wg, h->aux2));
+    h->wg_early = true;
+  }
   // the longest chains to host cores: k_hc_prep picks them (k_stats_long
   // skips them) ahead of the fork, so that `aux` holds nothing but
   // k_stats_long and its waves reach the CUs before the ingest grid of this
@@ -774,6 +800,10 @@ int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s) {
 }
 
 int stats_join(gk_set* h, hipStream_t s, const GKQuery& q) {
+  if (h->wg_early) {  // (run_ingest returned before joining the early k_ingest_wg)
+    h->wg_early = false;
+    HIP_TRY(hipStreamWaitEvent(s, h->ev_wg, 0));
+  }
   h->forked = false;
   HIP_TRY(hipStreamWaitEvent(s, h->ev_join, 0));
   if (h->presort_active) {
@@ -876,7 +906,7 @@ int run_ingest(gk_set* h, const double* x, const int64_t* offs, int force, hipSt
   // (a stream whose batches are not presorted -- no workspace yet, or it did
   // not fit -- is ranked unsorted there)
   const bool wg = prio && x != nullptr && h->ps.wg_count && h->aux2 && h->ps.list_ws;
-  if (wg) {
+  if (wg && !h->wg_early) {
     unsigned long long* wwork = work_counter(h, false);
     if (!wwork) return fail(GK_E_HIP, "no hand-out counter left for k_ingest_wg");
     // (behind k_long_prep, which counts its streams, and the call's counter
@@ -892,6 +922,7 @@ int run_ingest(gk_set* h, const double* x, const int64_t* offs, int force, hipSt
   // joined on every path once launched: the next call's begin_call zeroes the
   // counter block it adds to
   if (wg) HIP_TRY(hipStreamWaitEvent(stream, h->ev_wg, 0));
+  h->wg_early = false;
   HIP_TRY(lc);
   // (with k_ingest_wg beside it, the timed span is both: the call's batch ingest)
   hipEvent_t t1 = timed ? timing_event(h->tev_flush, h->n_flush) : nullptr;
@@ -1152,6 +1183,7 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
     }
     h->wg_trace = getenv("GK_WG_TRACE") != nullptr;
     okm &= hipEventCreateWithFlags(&h->ev_wg, hipEventDisableTiming) == hipSuccess;
+    okm &= hipEventCreateWithFlags(&h->ev_go, hipEventDisableTiming) == hipSuccess;
   }
   if (!okm) {
     gk_destroy(h);
@@ -1205,6 +1237,7 @@ int gk_destroy(gk_set* h) {
   if (h->aux3) (void)hipStreamDestroy(h->aux3);
   if (h->ev_presort) (void)hipEventDestroy(h->ev_presort);
   if (h->ev_wg) (void)hipEventDestroy(h->ev_wg);
+  if (h->ev_go) (void)hipEventDestroy(h->ev_go);
   for (double* p : h->hc_buf) (void)hipHostFree(p);
   if (h->aux) (void)hipStreamDestroy(h->aux);
   for (void* p : {(void*)h->h_ws_need, (void*)h->h_ovf, (void*)h->h_ctr, (void*)h->h_qs, (void*)h->h_hc,
@@ -1239,7 +1272,7 @@ int gk_ingest(gk_set* h, const double* values, const int64_t* offsets, void* str
   if (!rc) rc = take_sticky(h);
   if (!rc) rc = begin_call(h, s);
   if (rc) return rc;
-  rc = stats_fork(h, values, offsets, s);
+  rc = stats_fork(h, values, offsets, s, 0);
   if (rc) {
     stats_abort(h, s);
     return rc;
@@ -1357,7 +1390,7 @@ int gk_ingest_quantiles(gk_set* h, const double* values, const int64_t* offsets,
   rc = take_sticky(h);
   if (!rc) rc = begin_call(h, s);
   if (rc) return rc;
-  rc = stats_fork(h, values, offsets, s);
+  rc = stats_fork(h, values, offsets, s, 1);
   if (rc) {
     stats_abort(h, s);
     return rc;

@@ -382,7 +382,8 @@ __global__ __launch_bounds__(1024) void k_long_prep(GKState st, const int64_t* _
                                                     const int32_t* __restrict__ count,
                                                     int64_t* __restrict__ list_ws, int64_t* __restrict__ list_b0,
                                                     int64_t ws_cap, int64_t* __restrict__ ws_need,
-                                                    int32_t* __restrict__ wg_count, int wg_presort) {
+                                                    int32_t* __restrict__ wg_count, int wg_presort,
+                                                    int32_t* __restrict__ go) {
   __shared__ uint64_t key[GK_SORT_LONG_MAX];
   const int cnt = *count;
   const int t = threadIdx.x;
@@ -493,6 +494,16 @@ __global__ __launch_bounds__(1024) void k_long_prep(GKState st, const int64_t* _
     list_b0[i] = b;
     list_ws[i] = (nb > 0 && (b + nb) * st.P <= ws_cap) ? b * st.P : -1;
     b += nb;
+  }
+  // k_ingest_wg, launched ahead of this kernel (its workgroups hold their CUs
+  // before the chain walks and the presort fill the chip), waits for this
+  // word: every write above released first
+  if (go) {
+    __syncthreads();
+    if (t == 0) {
+      __threadfence();
+      __hip_atomic_store(go, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -2505,7 +2516,7 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
                                                        const double* __restrict__ psort,
                                                        const int64_t* __restrict__ prio_ws,
                                                        const int32_t* __restrict__ ps_done, int ps_grid,
-                                                       int hi_prio) {
+                                                       int hi_prio, const int32_t* __restrict__ go) {
   __shared__ WgLDS L;
   if (hi_prio) __builtin_amdgcn_s_setprio(3);  // (GK_WG_PRIO: the critical chains win the SIMD's issue arbitration)
 #ifdef GK_TIMELINE
@@ -2526,6 +2537,15 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
   const int t = threadIdx.x;
   if (t == 0) L.psflag_pub[0] = L.psflag_pub[1] = 0;
   const int P = st.P;
+  if (go) {
+    // launched ahead of k_long_prep (the stream list, the presort plan and
+    // this launch's stream count): wait for its word, then every thread
+    // acquires it (the list was written on another CU)
+    if (t == 0)
+      while (__hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) __builtin_amdgcn_s_sleep(8);
+    __syncthreads();
+    (void)__hip_atomic_load(go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+  }
   const int64_t K = *wg_count;
 #ifdef GK_PROF
   if (t == 0) {
@@ -5180,7 +5200,8 @@ hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x
 
 hipError_t gk_launch_ingest_wg(const GKState& st, const double* x, const int64_t* offs, const int32_t* long_list,
                                const int32_t* wg_count, int lcls, int force, int32_t* ovf_count, int32_t* ovf_list,
-                               unsigned long long* work, const GKPresort& ps, hipStream_t stream) {
+                               unsigned long long* work, const GKPresort& ps, hipStream_t stream,
+                               const int32_t* go) {
   if (st.S <= 0 || !ps.wg_count || !work) return hipSuccess;
   // (at most GK_WG_MAX streams: the count is only known on the device; the
   // spare workgroups find the hand-out exhausted and leave)
@@ -5190,7 +5211,7 @@ hipError_t gk_launch_ingest_wg(const GKState& st, const double* x, const int64_t
   static const int wg_prio = getenv("GK_WG_PRIO") ? atoi(getenv("GK_WG_PRIO")) : 1;
   hipLaunchKernelGGL(k_ingest_wg, dim3(GK_WG_MAX), dim3(GK_WG_T), 0, stream, st, x, offs, long_list, wg_count, lcls,
                      force, ovf_count, ovf_list, work, (const double*)ps.ws, (const int64_t*)ps.list_ws,
-                     (const int32_t*)ps.done, ps.done ? gk_presort_reg_grid(st) : 0, wg_prio);
+                     (const int32_t*)ps.done, ps.done ? gk_presort_reg_grid(st) : 0, wg_prio, go);
   return hipGetLastError();
 }
 
@@ -5207,11 +5228,11 @@ hipError_t gk_launch_stats(const GKState& st, const int64_t* offs, int32_t* long
 }
 
 hipError_t gk_launch_long_prep(const GKState& st, const int64_t* offs, int32_t* long_list, int64_t* long_n,
-                               int32_t* long_count, const GKPresort& ps, hipStream_t stream) {
+                               int32_t* long_count, const GKPresort& ps, hipStream_t stream, int32_t* go) {
   if (st.S <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_long_prep, dim3(1), dim3(1024), 0, stream, st, offs, long_list, long_n,
                      (const int32_t*)long_count, ps.list_ws, ps.list_b0, ps.ws_cap, ps.ws_need, ps.wg_count,
-                     ps.wg_presort);
+                     ps.wg_presort, go);
   return hipGetLastError();
 }
 

@@ -94,14 +94,15 @@ struct GKPresort {
 // (class lcls = 0 of the 2048 class only); the prio k_ingest launch skips them
 hipError_t gk_launch_ingest_wg(const GKState& st, const double* x, const int64_t* offs, const int32_t* long_list,
                                const int32_t* wg_count, int lcls, int force, int32_t* ovf_count, int32_t* ovf_list,
-                               unsigned long long* work, const GKPresort& ps, hipStream_t stream);
+                               unsigned long long* work, const GKPresort& ps, hipStream_t stream,
+                               const int32_t* go = nullptr);
 // the long-stream list + every stream's pre-call n (k_lengths)
 hipError_t gk_launch_stats(const GKState& st, const int64_t* offs, int32_t* long_list, int32_t* long_count,
                            hipStream_t stream);
 // the long list sorted longest first, the listed streams' pre-call n, the
 // presort plan and k_ingest_wg's stream count (k_long_prep)
 hipError_t gk_launch_long_prep(const GKState& st, const int64_t* offs, int32_t* long_list, int64_t* long_n,
-                               int32_t* long_count, const GKPresort& ps, hipStream_t stream);
+                               int32_t* long_count, const GKPresort& ps, hipStream_t stream, int32_t* go = nullptr);
 // gk:52-59 chains of the streams up to GK_STATS_LONG values (k_stats_short; the
 // long ones are k_stats_long's), when class 0 is not the small class
 hipError_t gk_launch_stats_short(const GKState& st, const double* x, const int64_t* offs, hipStream_t stream);
@@ -188,6 +189,7 @@ hipError_t gk_launch_promote(const GKState& st, const int32_t* list, int64_t cou
 #define GK_CTR_OVFC 40    // [40 + round]
 #define GK_CTR_BADPEND 48 // gk_import: streams with an unreachable pending count
 #define GK_CTR_WG 50      // k_ingest_wg's stream count this call (k_long_prep)
+#define GK_CTR_WGGO 53    // k_long_prep done: k_ingest_wg, launched ahead of it, starts its streams
 #define GK_CTR_PSDONE 51  // k_presort_reg's finished waves this call (k_ingest_wg beside it)
 #define GK_CTR_WORDS 18
 #define GK_CTR_CALL 16
