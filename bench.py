@@ -313,6 +313,10 @@ def main():
     if on_gpu:
         if rehearse:
             local %= max(torch.cuda.device_count(), 1)
+            if world > max(torch.cuda.device_count(), 1):
+                # ranks share a device: no rank's k_ingest_wg grid may spin on
+                # CUs ahead of its k_long_prep (GK_WG_EARLY, gk_capi.cpp)
+                os.environ.setdefault("GK_WG_EARLY", "0")
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
     else:
@@ -500,6 +504,23 @@ def main():
     k_ms = flush_ms / max(launches, 1)
     achieved = bytes_per_launch / (k_ms * 1e-3) / 1e9 if k_ms > 0 else None
     ratio = traffic / bytes_per_launch if traffic else None
+    per_rank = None
+    n_ranks = world
+    if world > 1:
+        # every rank's own launch time and algorithmic bytes; the headline
+        # roofline is the SLOWEST rank's launch on that rank's bytes (the node
+        # rate is bound by it), the others are listed beside it
+        import torch.distributed as dist
+        n_ranks = dist.get_world_size()  # the ranks that joined the process group
+        mine = {"rank": rank, "device": str(dev), "streams": S_loc, "values": N, "launch_ms": k_ms,
+                "bytes_per_launch": bytes_per_launch,
+                "frac": (bytes_per_launch / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if k_ms > 0 else None}
+        per_rank = [None] * n_ranks
+        dist.all_gather_object(per_rank, mine)
+        slow = max(per_rank, key=lambda r: r["launch_ms"])
+        k_ms, bytes_per_launch = slow["launch_ms"], slow["bytes_per_launch"]
+        achieved = bytes_per_launch / (k_ms * 1e-3) / 1e9 if k_ms > 0 else None
+        ratio = traffic / bytes_per_launch if traffic else None
     if a.workload == "cfg4":
         parallelism = ("row-sharded x%d, RCCL %s + merge" % (world, a.exchange) if K == 1 else
                        "row-sharded: %d virtual shards on 1 GPU, merge fold (no exchange)" % K)
@@ -528,7 +549,7 @@ def main():
         "metric": "values ingested/sec (node) @1M streams eps=0.01; % of HBM roofline",
         "value": value,
         "unit": "values/s",
-        "n_gpus": world,
+        "n_gpus": n_ranks,
         "steps": a.steps,
         "warmup": a.warmup,
         "warmup_run": {"steps": warm_info["steps"], "seconds": round(warm_info["seconds"], 4),
@@ -555,6 +576,11 @@ def main():
                      "stats_kernel_ms": stats_ms / max(launches, 1)},
         "library": _library_identity(),
     }
+    if per_rank is not None:
+        line["roofline"]["rank"] = slow["rank"]
+        line["roofline"]["per_rank"] = per_rank
+        line["roofline"]["note"] = ("N > 1: achieved / frac / launch_ms / bytes_per_launch of the slowest rank's "
+                                    "launch on that rank's own bytes; every rank under per_rank")
     if not on_gpu:
         line["device"] = "cpu (host engine libgkarray_cpu.so): a split check, not a GPU number"
     if world > 1 and split == "strong" and not a.no_weak:

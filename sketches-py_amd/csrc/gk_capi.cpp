@@ -101,6 +101,9 @@ struct gk_set {
     GKQuery q;
     bool may_defer = false;  // some class could run out of slots in it
   } last;
+  // a gk_reset came after the call whose counters are still in flight: its
+  // deferred streams are void (every stream was reset; nothing to re-run)
+  bool void_defer = false;
   int32_t fatal_seen = 0;  // device FATAL count already reported
   int sticky = GK_OK;      // asynchronous error reported by the next call / gk_sync
   std::string sticky_msg;
@@ -134,10 +137,10 @@ struct gk_set {
   int qs_n = 0;                // entries of the list last uploaded to d_qs (h_qs holds it)
   // eighths of a wave per CU of the small-class batch launch that walk the gk:52-59
   // stats chains first (0: separate k_stats launch); GK_FUSED_STATS overrides
-  int fused_stats = 7;
+  int fused_stats = 8;  // eighths of a wave per CU that start with the stats role (DESIGN 5 Stats)
   // gk_fold_packed: receives the packed states merged into this set (made on first use)
   gk_set* fold_scratch = nullptr;
-  gk_set* self_scratch = nullptr;  // snapshot source of dst.merge(dst), made on first use
+  gk_set* self_scratch = nullptr;  // snapshot source of dst.merge(dst), only during that merge
   // Host-walked chains: the gk:52-59 chains of the
   // longest streams run on host cores beside the GPU ingest.  hc_min: shortest
   // stream taken (0: off; GK_HOST_CHAINS=0 / GK_HOST_CHAIN_MIN); hc_threads:
@@ -285,6 +288,10 @@ void poll(gk_set* h, bool block) {
     return;
   }
   h->done_pending = false;
+  if (h->void_defer) {
+    h->h_ctr[GK_CTR_DEFER] = 0;
+    h->void_defer = false;
+  }
   if (h->ps.wg_count && h->wg_trace && h->h_ctr[GK_CTR_WORDS] > 0)
     fprintf(stderr, "[gk] k_ingest_wg: %d stream(s)\n", h->h_ctr[GK_CTR_WORDS]);
   const int32_t fatal = h->h_ctr[GK_CTR_FATAL];
@@ -453,6 +460,7 @@ int mark_done(gk_set* h, hipStream_t s) {
     HIP_TRY(hipMemcpyAsync(h->h_ctr + GK_CTR_WORDS, h->ps.wg_count, sizeof(int32_t), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipEventRecord(h->ev_done, s));
   h->done_pending = true;
+  h->void_defer = false;  // (the readback in flight is now this call's)
   return GK_OK;
 }
 
@@ -715,9 +723,15 @@ int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s, i
   // they found the CUs held by the chain walks and the presort and started
   // 3.1-4.2 ms into a 38.9 ms cfg5 call (profiles/r05/r05AF3_*).  Launched
   // only after k_long_prep is enqueued, so that the word is always written.
-  static const int early_env = getenv("GK_WG_EARLY") ? atoi(getenv("GK_WG_EARLY")) : 1;
+  // The early workgroups spin on the device until k_long_prep has run, so
+  // they are launched early only when the device keeps CUs free for it
+  // (gk_wg_early_ok: at least 2 x GK_WG_MAX CUs; a partitioned device or
+  // several sets sharing one could otherwise fill every CU with spinning
+  // workgroups).  Read per call, like the other GK_WG switches.
+  const char* early_s = getenv("GK_WG_EARLY");
+  const int early_env = early_s ? atoi(early_s) : 1;
   h->wg_early = false;
-  const bool early = early_env && x && h->ps.done && h->ps.wg_count && h->aux2 && h->ps.list_ws;
+  const bool early = early_env && x && h->ps.done && h->ps.wg_count && h->aux2 && h->ps.list_ws && gk_wg_early_ok();
   if (early) HIP_TRY(hipEventRecord(h->ev_go, s));
   // the long-stream list (k_lengths) + k_long_prep, then the fork
   // (k_stats_long needs only the sorted list and the pre-call n: the longest
@@ -1251,8 +1265,17 @@ int gk_reset(gk_set* h, void* stream) {
   int rc = check_set(h);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
-  rc = settle(h, s, false);  // a deferred re-run of the last call must not land after the reset
-  if (rc) return rc;
+  // No wait for the last call: streams it deferred for
+  // want of a slot would only be re-run to be reset; their re-run is void.
+  // (Waiting here put the host's enqueueing of every step on the GPU's
+  // critical path: ~90 us of idle GPU per step, 10 % of a 125k-stream rank
+  // share.)  The last call's counters are consumed when they arrive: its
+  // sticky errors are still reported, its deferred list is dropped.
+  hc_drain(h);  // (the host walk reads the last call's inputs)
+  poll(h, false);
+  if (h->done_pending) h->void_defer = true;
+  else h->h_ctr[GK_CTR_DEFER] = 0;
+  h->last.may_defer = false;
   // (k_reset puts every stream back in class 0: cls = slot = 0)
   // slots, member lists and re-run lists start over (FATAL stays cumulative:
   // a readback still in flight carries it)
@@ -1782,7 +1805,13 @@ static int merge_self(gk_set* dst, hipStream_t s, void* stream) {
   MergeArgsHost a{};
   a.src = dst->self_scratch->st;
   a.mode = 0;
-  return run_merge(dst, a, s);
+  rc = run_merge(dst, a, s);
+  // the snapshot set (a full copy of dst's state) is not kept beyond the
+  // merge: the set's memory stays what it was before
+  const int rs = gk_sync(dst, stream);
+  gk_destroy(dst->self_scratch);
+  dst->self_scratch = nullptr;
+  return rc ? rc : rs;
 }
 
 int gk_fold_packed(gk_set* dst, const void* const* bufs, int nbufs, void* stream) {
@@ -1809,10 +1838,15 @@ int64_t gk_host_chains_taken(gk_set* h) {
   // fail word when the worker reported a failure or its flag came too late
   // (the chains were then walked on the device: k_hc_fallback), even if the
   // worker finished OK afterwards
+  // (on the set's device, after the set's last call: ev_done follows its
+  // k_hc_wait; nothing else on the device is waited for -- ADVICE r05)
   int32_t dev_fail = 0;
-  if (hipDeviceSynchronize() != hipSuccess ||
-      hipMemcpy(&dev_fail, h->d_hc_fail, sizeof(dev_fail), hipMemcpyDeviceToHost) != hipSuccess)
-    return -1;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  bool ok = hipSetDevice(h->device) == hipSuccess && hipEventSynchronize(h->ev_done) == hipSuccess &&
+            hipMemcpy(&dev_fail, h->d_hc_fail, sizeof(dev_fail), hipMemcpyDeviceToHost) == hipSuccess;
+  (void)hipSetDevice(prev);
+  if (!ok) return -1;
   std::lock_guard<std::mutex> lk(h->hc_mu);
   return (h->hc_last_rc == GK_OK && dev_fail == 0) ? h->hc_last_taken : 0;
 }

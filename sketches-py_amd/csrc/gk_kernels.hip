@@ -21,6 +21,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <atomic>
 #include <limits>
 #include <type_traits>
 
@@ -3119,6 +3120,9 @@ __global__ __launch_bounds__(64) void k_ingest_big(GKState st, const double* __r
 //    prefix(g) + d - 1, one ballot + popcount per entry slot and quantile.
 // ===========================================================================
 #define SMALL_CAP GK_SMALL_CAP
+// values of one stream in one call that k_ingest_small takes (32-bit call
+// counters; the flush plan's (f + 63) * P stays below 2^31)
+#define GK_SMALL_LX_MAX (((int64_t)1 << 31) - ((int64_t)1 << 15))
 // Round-4 variants of the small class were measured on MI355X and removed
 // ((g, d) packed in 32 bits, T one flush ahead, selective
 // count zeroing, masked in-gap rank reads, every batch register-sorted).
@@ -3217,10 +3221,14 @@ static_assert(sizeof(int32_t) * (64 * 2 + 2) <= sizeof(int2) * 136, "mi fits in 
 // keeps a 4-VGPR zero alive across the flush and, short of registers, spills
 // it -- its reload's vmcnt wait then stalls on the in-flight LDS-DMA.)
 __device__ __forceinline__ void small_zero_counts(int2* gi, int lane) {
-  uint32_t z;
-  __asm__ volatile("v_mov_b32 %0, 0" : "=v"(z));
-  ((uint4*)gi)[lane] = make_uint4(z, z, z, z);           // records 0..127
-  ((uint2*)gi)[128 + (lane & 7)] = make_uint2(z, z);     // records 128..135
+  // two v_mov_b64 (a 4-VGPR zero for the 16-byte store, its low half for the
+  // 8-byte one), not one v_mov_b32 and five copies
+  typedef uint32_t gk_v4u __attribute__((ext_vector_type(4)));
+  gk_v4u z;
+  __asm__ volatile("v_mov_b64 %0, 0" : "=v"(z.xy));
+  __asm__ volatile("v_mov_b64 %0, 0" : "=v"(z.zw));
+  ((gk_v4u*)gi)[lane] = z;                                // records 0..127
+  ((uint2*)gi)[128 + (lane & 7)] = make_uint2(z.x, z.y);  // records 128..135
 }
 
 __device__ __forceinline__ void small_pad(double* tv, int E, int lane) {
@@ -3282,16 +3290,19 @@ __device__ __forceinline__ int gi_m(int x) { return (int)((uint32_t)x >> 24); }
 
 // One value x of a gap (its record gi) at rank `rk` inside the gap: gk:93-99
 // for an entry's gap, gk:85-92 for the tail.  Both rules evaluated, one store:
-// an absorbed value (or an empty slot, !valid) goes to the trash slot.
-// One value x of a gap (its record gi) at rank `rk` inside the gap: gk:93-99
-// for an entry's gap, gk:85-92 for the tail.  Both rules evaluated, one store:
 // an absorbed value (or an empty slot, !valid) goes to the trash slot.  (A
 // branch-free keep decision measured 14% slower on cfg3: the compiler's exec
 // branches skip the tail rule for most waves; profiles/r03f_ab_dma_emit_variants.txt.)
-template <int VPL>
+template <int VPL, bool NOTAIL = false>
 __device__ __forceinline__ void small_emit(SmallLDS<VPL>& L, bool in_gap, const CsDiv& cd, double x, int2 gi,
                                            int rk, bool valid) {
   const int k = gi_k(gi.x);
+  if constexpr (NOTAIL) {
+    // no value of the flush is in the tail gap (a wave-uniform fact): only
+    // the entry-gap rule, no chunk division
+    small_put<VPL, 8>(L, (valid && rk >= k) ? gi_ob(gi.x) + rk - k : GK_SMALL_TRASH, x, 1, gi.y);
+    return;
+  }
   const int q = cd.div(rk);
   const int rr = cd.rem(rk, q);
   const int pos = gi_ob(gi.x) + (in_gap ? rk - k : q);
@@ -3319,7 +3330,12 @@ template <int J>
 __device__ __forceinline__ double lane_xor_f64(double v, int lane) {
   // (round 4: one 64-bit DPP move per pair instead of two 32-bit ones saved a
   // v_mov per compare-exchange but gave wrong sorts on the GPU -- reverted)
-  return __hiloint2double(lane_xor_i32<J>(__double2hiint(v), lane), lane_xor_i32<J>(__double2loint(v), lane));
+  typedef int gk_v2i __attribute__((ext_vector_type(2)));
+  const gk_v2i a = __builtin_bit_cast(gk_v2i, v);
+  gk_v2i r;
+  r.x = lane_xor_i32<J>(a.x, lane);
+  r.y = lane_xor_i32<J>(a.y, lane);
+  return __builtin_bit_cast(double, r);
 }
 
 // a[r] against the value at lane ^ X (same r); the lower lane (bit LB of the
@@ -3327,6 +3343,31 @@ __device__ __forceinline__ double lane_xor_f64(double v, int lane) {
 template <int X, int LB>
 __device__ __forceinline__ void cx_stage2(double (&a)[2], int lane) {
   const bool lower = (lane & LB) == 0;
+  if constexpr (X == LB && (X == 16 || X == 32)) {
+    // lane ^ 16 / lane ^ 32 by ONE permlane swap per half and no partner
+    // select: the swap of (A, B) = (a, a) leaves A = own, B = partner in the
+    // lower rows (halves) and A = partner, B = own in the upper ones, so
+    // "B < A" decides both sides: lower keeps B iff B < A (the min), upper
+    // keeps B iff not (the max); equal keys are bit-identical.
+    typedef int gk_v2i __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const gk_v2i v = __builtin_bit_cast(gk_v2i, a[r]);
+      gk_v2i A, B;
+      if constexpr (X == 16) {
+        const auto lo = __builtin_amdgcn_permlane16_swap(v.x, v.x, false, false);
+        const auto hi = __builtin_amdgcn_permlane16_swap(v.y, v.y, false, false);
+        A.x = (int)lo[0]; B.x = (int)lo[1]; A.y = (int)hi[0]; B.y = (int)hi[1];
+      } else {
+        const auto lo = __builtin_amdgcn_permlane32_swap(v.x, v.x, false, false);
+        const auto hi = __builtin_amdgcn_permlane32_swap(v.y, v.y, false, false);
+        A.x = (int)lo[0]; B.x = (int)lo[1]; A.y = (int)hi[0]; B.y = (int)hi[1];
+      }
+      const double da = __builtin_bit_cast(double, A), db = __builtin_bit_cast(double, B);
+      a[r] = ((db < da) == lower) ? db : da;
+    }
+    return;
+  }
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
     const double p = lane_xor_f64<X>(a[r], lane);
@@ -3938,8 +3979,15 @@ __device__ __forceinline__ int flush_small(SmallLDS<VPL>& L, const int E, const 
           }
       }
     }
+    // (mE: the tail gap's members.  Most flushes have none -- a value past
+    // the table's last entry is a new maximum -- and skip the tail rule.)
+    if (mE == 0) {
 #pragma unroll
-    for (int r = 0; r < VPL; ++r) small_emit(L, xb[r] < pE8, cd, xv[r], gv[r], rk[r], lane + 64 * r < cnt);
+      for (int r = 0; r < VPL; ++r) small_emit<VPL, true>(L, true, cd, xv[r], gv[r], rk[r], lane + 64 * r < cnt);
+    } else {
+#pragma unroll
+      for (int r = 0; r < VPL; ++r) small_emit(L, xb[r] < pE8, cd, xv[r], gv[r], rk[r], lane + 64 * r < cnt);
+    }
     GK_MARK(L, 5);
   } else {
     // A large gap (the first flush, where every value is tail, or an
@@ -4098,6 +4146,9 @@ __device__ __attribute__((noinline)) double small_quantiles(SmallLDS<VPL>& L, in
 #ifndef GK_FS_DEPTH
 #define GK_FS_DEPTH 2  // chunks of 8 values in flight per lane
 #endif
+#ifndef GK_FS_VMINMAX
+#define GK_FS_VMINMAX 0
+#endif
 #define GK_SWORK_IDX 128  // the stats batch counters in `work` (after the 8 ingest parts), one per part
 #ifndef GK_FS_LAG_DEFAULT
 #define GK_FS_LAG_DEFAULT 256  // streams the ingest hand-out runs ahead of a stats batch (GK_FS_LAG overrides)
@@ -4195,15 +4246,39 @@ __device__ __forceinline__ void fused_stats_role(const GKState& st, const double
           const int64_t c = c0 + d;
           if (c < nch) {
             const double* __restrict__ rt = st.rtab + (nu + 8 * c + 1);  // uniform (TAB)
+#if GK_FS_VMINMAX
+            const double mn0 = mn, mx0 = mx;
+#endif
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
               const double v = (k & 1) ? ring[d][k >> 1].y : ring[d][k >> 1].x;
               const double rc = TAB ? rt[k] : 1.0 / (double)(n + 1 + k);  // off the chain
               sm = sm + v;                    // gk:53
               av = av + (v - av) * rc;        // gk:54
+#if GK_FS_VMINMAX
+              // one v_min_f64 / v_max_f64 each (no NaN inputs): the
+              // strict compares of gk:56-59 differ from them only in which
+              // zero a minimum / maximum of +-0 keeps -- redone below
+              __asm__("v_min_f64 %0, %1, %2" : "=v"(mn) : "v"(v), "v"(mn));
+              __asm__("v_max_f64 %0, %1, %2" : "=v"(mx) : "v"(v), "v"(mx));
+#else
               if (v < mn) mn = v;             // gk:56-57
               if (v > mx) mx = v;             // gk:58-59
+#endif
             }
+#if GK_FS_VMINMAX
+            if (__builtin_amdgcn_ballot_w64(mn == 0.0 || mx == 0.0) != 0) {
+              // a zero extreme: the chunk's gk:56-59 again, strictly, in order
+              mn = mn0;
+              mx = mx0;
+#pragma unroll
+              for (int k = 0; k < 8; ++k) {
+                const double v = (k & 1) ? ring[d][k >> 1].y : ring[d][k >> 1].x;
+                if (v < mn) mn = v;
+                if (v > mx) mx = v;
+              }
+            }
+#endif
             n += 8;                           // gk:52
           }
           const int64_t nx = c + DEPTH;
@@ -4323,9 +4398,11 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
     if (Lx <= 0 && !((force == 1 && p > 0) || (force == 2 && n > 0)) && !qs) continue;
     GKRec* __restrict__ tab = gk_table_ptr_cs(st, s, scls, sslot);
     double* __restrict__ pb = st.pbuf + s * (int64_t)st.pmax;
-    // an imported / merged table without room for the padding, or a stream
-    // past the count limit: promotion
-    bool ok = E <= SMALL_CAP - 1 && gk_count_ok(st, n + (Lx > 0 ? Lx : 0));
+    // an imported / merged table without room for the padding, a stream
+    // past the count limit, or one with 2^31 - 2^15 or more values in this
+    // call (the flush loop counts in 32 bits; k_ingest counts in 64):
+    // promotion
+    bool ok = E <= SMALL_CAP - 1 && gk_count_ok(st, n + (Lx > 0 ? Lx : 0)) && Lx < GK_SMALL_LX_MAX;
     if (ok) {
       // 16-byte records moved as int4: all loads issued before the first wait
       const int4* __restrict__ t4 = (const int4*)tab;
@@ -4349,44 +4426,64 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
 
     bool flushed = false;  // at least one flush in this call
     bool final_done = false;
-    int64_t used = 0;
-    int64_t need = P - (n % P);  // adds until n hits the next multiple of P (gk:60)
-    // float(n - 1) of gk:70, kept as a double that each flush advances by
-    // its adds (integers < 2^53: exact); T = floor((2 eps) * (n - 1)) is then
-    // a multiply and a truncation (n >= 1 at every flush, and gk_count_ok
-    // above bounds T by GK_T_CLAMP for the whole call: no clamps)
-    double nm1 = (double)(n - 1);
+    // Per-call counters in 32 bits (ok: Lx < GK_SMALL_LX_MAX), so that the
+    // loop's tests are scalar compares, not 64-bit VALU ones.
+    const int L32 = (int)Lx;
+    int used = 0;
+    const int need0 = P - (int)(n % P);  // adds until n hits the next multiple of P (gk:60)
+    int need = need0;
+    // T = floor((2 eps) * float(n - 1)) (gk:70) and the chunk divider of
+    // every flush of the call, 64 flushes at a time, lane f for flush f: n at
+    // flush f is n + min(need0 + f P, Lx) (the last term for the requested
+    // flush that ends the call), float(n - 1) exact (integers < 2^53), and
+    // gk_count_ok above bounds T by GK_T_CLAMP (no clamps).  The flush reads
+    // its T and magic number with two v_readlane.
+    const double nm1c = (double)(n - 1);
+    int fl = 0;  // flushes made in this call
+    int tT = 0;
+    uint32_t tM = 0;
+    auto plan_t = [&]() {
+      const int k = min(need0 + (fl + lane) * P, L32);
+      tT = (int)(st.two_eps * (nm1c + (double)k));
+      const uint32_t cs = (uint32_t)max(tT, 1);
+      tM = cs < 256u ? ((1u << 23) + cs - 1u) / cs : 1u;
+    };
+    // the stream's values from x + xo as a buffer resource: the prefetch of
+    // the next flush reads lanes past its count as 0 (range check), with no
+    // address clamps or 64-bit address arithmetic on the VALU
+    const double* const xs = x ? x + xo : pb;
     double xv[VPL];
 #pragma unroll
     for (int r = 0; r < VPL; ++r) xv[r] = 0.0;
     while (ok) {
-      const bool autof = used + need <= Lx;
-      int64_t nadd;
+      const bool autof = need <= L32 - used;
+      int nadd;
       if (autof) {
         nadd = need;
       } else {
-        nadd = Lx - used;  // < need: only a requested flush takes these now
+        nadd = L32 - used;  // < need: only a requested flush takes these now
         if (!((force == 1 && p + nadd > 0) || force == 2)) break;
       }
-      const int cnt = p + (int)nadd;
-      if (!flushed) gk_load_flush_values<VPL>(xv, pb, p, x ? x + xo + used : pb, cnt, lane);
-      const int64_t nused = used + nadd;
+      const int cnt = p + nadd;
+      if (!flushed) gk_load_flush_values<VPL>(xv, pb, p, xs, cnt, lane);
+      const int nused = used + nadd;
       // the next flush's values (or the leftover tail), loaded one flush ahead
-      const int navail = autof ? (int)min((int64_t)P, Lx - nused) : 0;
+      const int navail = autof ? min(P, L32 - nused) : 0;
       double xn[VPL];
-#pragma unroll
-      for (int r = 0; r < VPL; ++r) xn[r] = 0.0;
       auto prefetch = [&]() {
-        if (navail > 0) {
-          const double* base = x + xo + nused;
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(xs + nused), 0, navail * (int)sizeof(double), 0x00020000);
 #pragma unroll
-          for (int r = 0; r < VPL; ++r) xn[r] = base[min(lane + 64 * r, navail - 1)];
-        }
+        for (int r = 0; r < VPL; ++r)
+          xn[r] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, (lane + 64 * r) * 8, 0, 0));
       };
+      if ((fl & 63) == 0) plan_t();
       n += nadd;
-      nm1 += (double)(int)nadd;
-      const int T = __builtin_amdgcn_readfirstlane((int)(st.two_eps * nm1));
-      const CsDiv cd = make_csdiv(T);
+      const int T = __builtin_amdgcn_readlane(tT, fl & 63);
+      CsDiv cd;
+      cd.cs = max(T, 1);
+      cd.m = (uint32_t)__builtin_amdgcn_readlane((int)tM, fl & 63);
+      ++fl;
       // (profiling builds: the loop top of a wave's FIRST stream counts apart, in 11)
       GK_MARK(L, (GK_PROF_FIRST && !prof_done_any) ? 11 : 8);
       int nE;
@@ -4406,7 +4503,7 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
       need = P;
       flushed = true;
 #pragma unroll
-      for (int r = 0; r < VPL; ++r) xv[r] = (lane + 64 * r < navail) ? xn[r] : 0.0;
+      for (int r = 0; r < VPL; ++r) xv[r] = xn[r];  // 0.0 past navail (range check)
       GK_MARK(L, 10);  // (profiling builds: the wait for the prefetched values)
       if (!autof) {
         final_done = true;
@@ -4414,15 +4511,15 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
       }
     }
     if (ok && !final_done) {
-      const int64_t rem = Lx - used;  // < need: stays pending
+      const int rem = L32 - used;  // < need: stays pending
       if (flushed) {
 #pragma unroll
         for (int r = 0; r < VPL; ++r)
           if (lane + 64 * r < rem) pb[lane + 64 * r] = xv[r];
       } else {
-        for (int64_t i = lane; i < rem; i += 64) pb[p + i] = x[xo + used + i];
+        for (int i = lane; i < rem; i += 64) pb[p + i] = xs[used + i];
       }
-      p += (int)rem;
+      p += rem;
       n += rem;
     }
     // the table (E <= 127: two records per lane, all LDS reads before the
@@ -5052,20 +5149,41 @@ __global__ void k_promote_dev(GKState st, const int32_t* __restrict__ count, con
 // ===========================================================================
 // host-side launchers (called from gk_capi.cpp)
 // ===========================================================================
-static int g_num_cu = 0;
+// Host-side values cached per device (a set's calls run on its own device,
+// made current by the caller): the CU count and each launcher's occupancy
+// query (a host API call of several us), one relaxed atomic slot per device.
+#define GK_MAX_DEV 64
+template <typename Q>
+static int per_device(std::atomic<int> (&cache)[GK_MAX_DEV], Q query) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::atomic<int>& c = cache[(unsigned)dev % GK_MAX_DEV];
+  int v = c.load(std::memory_order_relaxed);
+  if (v <= 0) {
+    v = query(dev);
+    if (v <= 0) v = 1;
+    c.store(v, std::memory_order_relaxed);
+  }
+  return v;
+}
 
 static int num_cu() {
-  if (g_num_cu == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
+  static std::atomic<int> cache[GK_MAX_DEV];
+  return per_device(cache, [](int dev) {
     hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, dev) == hipSuccess) g_num_cu = prop.multiProcessorCount;
-    if (g_num_cu <= 0) g_num_cu = 256;
-  }
-  return g_num_cu;
+    return hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0 ? prop.multiProcessorCount
+                                                                                           : 256;
+  });
 }
 
 int gk_num_cu() { return num_cu(); }
+
+// GK_WG_EARLY: k_ingest_wg's GK_WG_MAX workgroups (one per CU: 128 KiB of
+// LDS each) are launched ahead of k_long_prep and spin until it has run, so
+// the device must keep CUs free for it: at least as many again as the early
+// grid holds (else the call launches them behind k_long_prep, as with
+// GK_WG_EARLY=0).
+int gk_wg_early_ok() { return num_cu() >= 2 * GK_WG_MAX; }
 
 template <int CAP, int VPL>
 static hipError_t launch_ingest_t(const GKState& st, const double* x, const int64_t* offs,
@@ -5081,11 +5199,12 @@ static hipError_t launch_ingest_t(const GKState& st, const double* x, const int6
   if (CAP > 0) {
     // one resident wave per slot; streams are handed out through `work`
     // (the occupancy query is a host API call of several us: once per kernel)
-    static int occ = 0;
-    if (occ <= 0) {
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_ingest<CAP, VPL>, 64, 0);
-      if (occ <= 0) occ = 1;
-    }
+    static std::atomic<int> occ_cache[GK_MAX_DEV];
+    const int occ = per_device(occ_cache, [](int) {
+      int o = 0;
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_ingest<CAP, VPL>, 64, 0);
+      return o;
+    });
     grid = (int64_t)num_cu() * occ;
   } else {
     grid = ws_blocks;
@@ -5126,11 +5245,12 @@ static hipError_t launch_ingest_small(const GKState& st, const double* x, const 
                                       hipStream_t stream) {
   if (count <= 0) return hipSuccess;
   if (!work) return hipErrorInvalidValue;
-  static int occ = 0;  // (queried once: a host API call of several us)
-  if (occ <= 0) {
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_ingest_small<VPL, false>, 64, 0);
-    if (occ <= 0) occ = 1;
-  }
+  static std::atomic<int> occ_cache[GK_MAX_DEV];  // (queried once per device)
+  const int occ = per_device(occ_cache, [](int) {
+    int o = 0;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_ingest_small<VPL, false>, 64, 0);
+    return o;
+  });
   // one resident wave per slot; streams are handed out through `work`
   int64_t grid = (int64_t)num_cu() * occ;
   if (grid > count) grid = count;

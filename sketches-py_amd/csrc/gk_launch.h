@@ -39,6 +39,8 @@ struct MergeArgsHost {
 };
 
 int gk_num_cu();
+// the device has CUs to spare for k_long_prep beside an early k_ingest_wg grid
+int gk_wg_early_ok();
 size_t gk_ingest_ws_bytes(int cap, int vpl);
 // k_ingest_big (any capacity, any flush period): bytes of one block's workspace
 size_t gk_big_ws_bytes(int cap, int P);

@@ -60,6 +60,17 @@ def check_split(tmp_path, args, S, world, device_args, env_extra=None, launcher=
     line = run_bench(args + device_args, world, str(tmp_path / "split"), env_extra, launcher)
     assert line["scaling"] == "strong" and line["config"]["split"] == "strong" and line["n_gpus"] == world
     assert "weak" in line and line["weak"]["scaling"] == "weak"
+    # N > 1: every rank's launch under roofline.per_rank,
+    # the headline roofline = the slowest rank's launch on that rank's bytes
+    rf = line["roofline"]
+    pr = rf["per_rank"]
+    assert [r["rank"] for r in pr] == list(range(world))
+    assert sum(r["streams"] for r in pr) == S and sum(r["values"] for r in pr) > 0
+    slow = max(pr, key=lambda r: r["launch_ms"])
+    assert rf["rank"] == slow["rank"] and rf["launch_ms"] == slow["launch_ms"]
+    assert rf["bytes_per_launch"] == slow["bytes_per_launch"]
+    if slow["launch_ms"] > 0:
+        assert abs(rf["frac"] - slow["frac"]) <= 1e-12 * max(1.0, abs(slow["frac"]))
     q1 = np.load(str(tmp_path / "one") + ".rank0.npz")["q"]
     qn, parts = gather(str(tmp_path / "split"), world, S)
     assert np.array_equal(q1.view(np.int64), qn.view(np.int64)), "strong split changed some stream's quantiles"

@@ -8,7 +8,7 @@ import pytest
 import torch
 
 from gk_oracle_c import OracleSet
-from parity_util import _ss, assert_same_quantiles, assert_same_state, csr, gen, small_of
+from parity_util import _ss, assert_same_quantiles, assert_same_state, assert_same_tables, csr, gen, small_of
 
 pytestmark = pytest.mark.gpu
 
@@ -136,6 +136,61 @@ def test_unbounded_class_after_32768_ladder(gpu_device, monkeypatch, caps):
     seqs = [desc(n), rng.random(20000), np.arange(3000, dtype=np.float64), rng.pareto(1.5, 50000) + 1]
     run_batches(ss, o, [seqs, [s[: len(s) // 3] for s in seqs]], "ladder " + caps)
     check_q(ss, o, eps, "ladder " + caps)
+
+
+@pytest.mark.parametrize("caps", ["128,4096b", "128,2048,4096b"])
+def test_small_class_partial_commit_then_promotion(gpu_device, monkeypatch, caps):
+    """k_ingest_small commits the flushes of a call that fit its 128 entries
+    and the promoted stream continues in the next class from value n - n0 of
+    the call: a descending stream at eps = 0.01 flushes several
+    times in class 0 before it outgrows it (462 entries after 20 000 values),
+    in one call and over calls, into k_ingest<2048> or straight into
+    k_ingest_big; beside it streams that stay small.  Bit-exact vs the
+    oracle after every call."""
+    monkeypatch.setenv("GK_CAPS", caps)
+    eps = 0.01
+    rng = np.random.default_rng(17)
+    ss = _ss(5, eps, gpu_device)
+    o = OracleSet(5, eps)
+    d = desc(20000)
+    b1 = [d[:6000], rng.random(3000), d[:250], rng.pareto(1.5, 999) + 1, np.zeros(0)]
+    b2 = [d[6000:], rng.random(1234), d[250:20000] - 1e6, rng.pareto(1.5, 5000) + 1, d[:40]]
+    run_batches(ss, o, [b1, b2], "partial commit " + caps)
+    assert ss.num_promoted >= 2
+    check_q(ss, o, eps, "partial commit " + caps)
+
+
+def test_small_class_fatal_stream_keeps_committed_prefix(gpu_device, monkeypatch):
+    """A stream that outgrows every class (GK_CAPS=128,256: no unbounded
+    class) is reported (sticky GK_E_OVERFLOW); what it keeps is the state
+    after the last flush that fitted the small class -- exactly the oracle's
+    state after that prefix of its values (a flush boundary: no pending
+    value) -- and the other streams of the call are added in full."""
+    monkeypatch.setenv("GK_CAPS", "128,256")
+    eps = 0.01
+    rng = np.random.default_rng(23)
+    ss = _ss(3, eps, gpu_device)
+    d = desc(20000)
+    seqs = [rng.random(5000), d, rng.pareto(1.5, 777) + 1]
+    flat, offs = csr(seqs)
+    ss.ingest(torch.from_numpy(flat), torch.from_numpy(offs), sync=False)
+    with pytest.raises(Exception, match="outgrew"):
+        ss.sync()
+    st = {k: v.cpu().numpy() for k, v in ss.stats().items()}
+    n1 = int(st["n"][1])
+    P = int(1 / eps) + 1
+    assert 0 < n1 < d.size and n1 % P == 0 and int(st["pending"][1]) == 0
+    o = OracleSet(3, eps)
+    o.ingest(*csr([seqs[0], d[:n1], seqs[2]]))
+    assert_same_tables(ss, o, what="fatal prefix")
+    ost = o.stats()
+    for k in ("n", "size", "pending"):
+        assert np.array_equal(st[k].astype(np.int64), ost[k].astype(np.int64)), "fatal prefix " + k
+    # (min/max/sum/avg of the refused call's values are computed beside the
+    # tables and include them -- DESIGN 4's documented deviation (3); the
+    # other streams' are exact)
+    for k in ("min", "max", "sum", "avg"):
+        assert np.array_equal(st[k][[0, 2]].view(np.int64), ost[k][[0, 2]].view(np.int64)), "other streams " + k
 
 
 def test_merge_tiny_eps_vs_oracle(gpu_device):

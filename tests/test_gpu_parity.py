@@ -143,6 +143,32 @@ def test_dropin_self_merge(gpu_device):
     assert_same_state(b, ob, "repeated source")
 
 
+def test_self_merge_promoted_streams_eps_0001(gpu_device):
+    """a.merge(a) at eps = 0.001 (P = 1001: no small class) with streams
+    promoted out of class 0 (descending streams: thousands of entries, the
+    32768 class) beside short ones: the snapshot path of merge_self in the
+    larger classes, twice in a row (its scratch set is made and released per
+    merge), bit-exact vs the oracle."""
+    rng = np.random.default_rng(31)
+    eps = 0.001
+    seqs = [np.arange(300000, 0, -1, dtype=np.float64), rng.random(50000), rng.lognormal(0, 1, 5000),
+            np.zeros(0), np.arange(30000, 0, -1, dtype=np.float64) * 0.5, rng.pareto(1.5, 2999) + 1]
+    a, oa = _ss(len(seqs), eps, gpu_device), OracleSet(len(seqs), eps)
+    ingest_np(a, seqs)
+    oa.ingest(*csr(seqs))
+    assert a.num_promoted >= 1
+    a.merge_from([a])
+    oa.merge(oa)
+    assert_same_state(a, oa, "self-merge eps=.001")
+    more = [rng.random(int(L)) for L in rng.integers(0, 4000, len(seqs))]
+    ingest_np(a, more)
+    oa.ingest(*csr(more))
+    a.merge_from([a, a])
+    oa.merge(oa)
+    oa.merge(oa)
+    assert_same_state(a, oa, "self-merge twice eps=.001")
+
+
 def test_eps_mismatch(gpu_device):
     from gkarray_amd import UnequalEpsilonException
     a = _ss(4, 0.01, gpu_device)

@@ -69,16 +69,17 @@ def run(dev, monkeypatch, env, calls):
     return ss, res
 
 
-@pytest.mark.parametrize("presort,conc", [("1", "1"), ("1", "0"), ("0", "1")])
-def test_wg_streams_match_oracle_and_one_wave_path(gpu_device, monkeypatch, capfd, presort, conc):
+@pytest.mark.parametrize("presort,conc,early", [("1", "1", "1"), ("1", "1", "0"), ("1", "0", "1"), ("0", "1", "1")])
+def test_wg_streams_match_oracle_and_one_wave_path(gpu_device, monkeypatch, capfd, presort, conc, early):
     """presort 1, conc 1 (the default): presorted batches from the presort
     running beside the workgroups; conc 0: the presort ahead of them;
     presort 0: k_ingest_wg ranks every batch among its gaps' members (and
     sorts a batch with a crowded gap: the descending stream's batches all
-    fall below the table)."""
+    fall below the table).  early 1 (the default): the workgroups launched
+    ahead of k_long_prep, spinning on its word; early 0: behind it."""
     calls = batches(5)
     ss, res = run(gpu_device, monkeypatch, {"GK_WG": "1", "GK_WG_TRACE": "1", "GK_WG_PRESORT": presort,
-                                            "GK_WG_CONC": conc}, calls)
+                                            "GK_WG_CONC": conc, "GK_WG_EARLY": early}, calls)
     err = capfd.readouterr().err
     took = [int(m) for m in re.findall(r"k_ingest_wg: (\d+) stream", err)]
     assert took and max(took) > 0, "k_ingest_wg took no stream: %r" % err[-2000:]

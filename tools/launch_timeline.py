@@ -117,6 +117,11 @@ def main():
         print("%s (%s warm-up steps): %d waves, %d streams stamped; launch (first wave start -> last wave end) %.1f us"
               % (arg, os.environ.get("TL_WARM", "4"), len(w), ok.sum(), T))
         print("  wave start        ", pct(ws))
+        bidx = np.nonzero(wave.reshape(-1, 5)[:, 0] > 0)[0]
+        late = ws > 100.0
+        if late.any():
+            print("  late waves (start > 100 us): %d, blockIdx %s, their stats-role end %s, end %s"
+                  % (late.sum(), pct(bidx[late]), pct(wr[late]), pct(we[late])))
         # the shader clock over each wave's life: s_memtime ticks / s_memrealtime ticks x 100 MHz
         clk = (w[:, 4] - w[:, 3]) / np.maximum(w[:, 2] - w[:, 0], 1) * 100.0
         print("  shader clock MHz  ", pct(clk))
