@@ -4146,9 +4146,6 @@ __device__ __attribute__((noinline)) double small_quantiles(SmallLDS<VPL>& L, in
 #ifndef GK_FS_DEPTH
 #define GK_FS_DEPTH 2  // chunks of 8 values in flight per lane
 #endif
-#ifndef GK_FS_VMINMAX
-#define GK_FS_VMINMAX 0
-#endif
 #define GK_SWORK_IDX 128  // the stats batch counters in `work` (after the 8 ingest parts), one per part
 #ifndef GK_FS_LAG_DEFAULT
 #define GK_FS_LAG_DEFAULT 256  // streams the ingest hand-out runs ahead of a stats batch (GK_FS_LAG overrides)
@@ -4246,39 +4243,15 @@ __device__ __forceinline__ void fused_stats_role(const GKState& st, const double
           const int64_t c = c0 + d;
           if (c < nch) {
             const double* __restrict__ rt = st.rtab + (nu + 8 * c + 1);  // uniform (TAB)
-#if GK_FS_VMINMAX
-            const double mn0 = mn, mx0 = mx;
-#endif
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
               const double v = (k & 1) ? ring[d][k >> 1].y : ring[d][k >> 1].x;
               const double rc = TAB ? rt[k] : 1.0 / (double)(n + 1 + k);  // off the chain
               sm = sm + v;                    // gk:53
               av = av + (v - av) * rc;        // gk:54
-#if GK_FS_VMINMAX
-              // one v_min_f64 / v_max_f64 each (no NaN inputs): the
-              // strict compares of gk:56-59 differ from them only in which
-              // zero a minimum / maximum of +-0 keeps -- redone below
-              __asm__("v_min_f64 %0, %1, %2" : "=v"(mn) : "v"(v), "v"(mn));
-              __asm__("v_max_f64 %0, %1, %2" : "=v"(mx) : "v"(v), "v"(mx));
-#else
               if (v < mn) mn = v;             // gk:56-57
               if (v > mx) mx = v;             // gk:58-59
-#endif
             }
-#if GK_FS_VMINMAX
-            if (__builtin_amdgcn_ballot_w64(mn == 0.0 || mx == 0.0) != 0) {
-              // a zero extreme: the chunk's gk:56-59 again, strictly, in order
-              mn = mn0;
-              mx = mx0;
-#pragma unroll
-              for (int k = 0; k < 8; ++k) {
-                const double v = (k & 1) ? ring[d][k >> 1].y : ring[d][k >> 1].x;
-                if (v < mn) mn = v;
-                if (v > mx) mx = v;
-              }
-            }
-#endif
             n += 8;                           // gk:52
           }
           const int64_t nx = c + DEPTH;
@@ -4485,7 +4458,9 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
       cd.m = (uint32_t)__builtin_amdgcn_readlane((int)tM, fl & 63);
       ++fl;
       // (profiling builds: the loop top of a wave's FIRST stream counts apart, in 11)
-      GK_MARK(L, (GK_PROF_FIRST && !prof_done_any) ? 11 : 8);
+      // (GK_PROF_FIRST 1: a wave's first stream's loop tops; 2: every
+      // stream's first loop top -- its first values' load -- in section 11)
+      GK_MARK(L, (GK_PROF_FIRST == 2 ? !flushed : (GK_PROF_FIRST && !prof_done_any)) ? 11 : 8);
       int nE;
       if constexpr (SMALL_CAP > 128)
         nE = E <= 127 ? flush_small<VPL, 2>(L, E, xv, cnt, T, cd, lane, prefetch)
