@@ -752,12 +752,13 @@ int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s, i
   if (prep)
     HIP_TRY(gk_launch_long_prep(h->st, offs, h->d_long_list, h->d_long_n, h->d_long_count, h->ps, s,
                                 early ? h->d_ctr + GK_CTR_WGGO : nullptr));
+  unsigned long long* wwork_early = nullptr;
   if (early && prep) {
-    unsigned long long* wwork = work_counter(h, false);
-    if (!wwork) return fail(GK_E_HIP, "no hand-out counter left for k_ingest_wg");
+    wwork_early = work_counter(h, false);
+    if (!wwork_early) return fail(GK_E_HIP, "no hand-out counter left for k_ingest_wg");
     HIP_TRY(hipStreamWaitEvent(h->aux2, h->ev_go, 0));
     HIP_TRY(gk_launch_ingest_wg(h->st, x, offs, h->d_long_list, h->ps.wg_count, 0, force, ovf_count(h, 0),
-                                ovf_list(h, 0), wwork, h->ps, h->aux2, h->d_ctr + GK_CTR_WGGO));
+                                ovf_list(h, 0), wwork_early, h->ps, h->aux2, h->d_ctr + GK_CTR_WGGO));
     HIP_TRY(hipEventRecord(h->ev_wg, h->aux2));
     h->wg_early = true;
   }
@@ -786,6 +787,16 @@ int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s, i
     h->hc_offs = offs;
   }
   HIP_TRY(hipEventRecord(h->ev_fork, s));
+  if (wwork_early) {
+    // behind k_long_prep, on the same hand-out counter: the streams of any
+    // early workgroup that gave up waiting for k_long_prep's word (bounded
+    // spin, GK_WG_GO_TICKS); normally none are left and its workgroups leave
+    // at once
+    HIP_TRY(hipStreamWaitEvent(h->aux2, h->ev_fork, 0));
+    HIP_TRY(gk_launch_ingest_wg(h->st, x, offs, h->d_long_list, h->ps.wg_count, 0, force, ovf_count(h, 0),
+                                ovf_list(h, 0), wwork_early, h->ps, h->aux2, nullptr));
+    HIP_TRY(hipEventRecord(h->ev_wg, h->aux2));
+  }
   HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_fork, 0));
   h->forked = true;
   HIP_TRY(gk_launch_stats_long(h->st, x, offs, h->d_long_list, prep ? h->d_long_n : nullptr, h->d_long_count,

@@ -1982,7 +1982,33 @@ struct WgLDS {
   alignas(16) int32_t xbig[GK_WG_WAVES];  // per wave: a gap with GK_WG_RANK_MAX members or more
   alignas(16) int32_t xcrowd[GK_WG_WAVES];  // per wave: a thread with > GK_WG_EMIT_MAX gap survivors
   uint32_t total;
+  int go_ok;  // k_ingest_wg launched early: k_long_prep's word came in time
 };
+#ifndef GK_WG_GO_TICKS
+#define GK_WG_GO_TICKS 100000000ull  // 1 s of s_memrealtime (100 MHz)
+#endif
+
+// The workgroup flush's value table in BFS (Eytzinger) order (GK_WG_EYTZ):
+// sorted position j (0-based) of a table padded to 2^H - 1 entries lives at
+// node (j + 1 + 2^H) >> (ctz(j + 1) + 1), the root at 1.  A search level's
+// probes are then one contiguous row of nodes (2^l of them), so lanes with
+// different values hit consecutive slots -- distinct LDS banks -- where the
+// sorted layout's probes of a deep level are 2^(H-l) slots apart and share
+// one bank (the 423 conflict cycles per wave and flush of round 5).
+#ifndef GK_WG_EYTZ
+#define GK_WG_EYTZ 1
+#endif
+__device__ __forceinline__ int wg_slot(int j, int H) {
+#if GK_WG_EYTZ
+  const int p1 = j + 1;
+  return (p1 + (1 << H)) >> (__builtin_ctz((unsigned)p1) + 1);
+#else
+  (void)H;
+  return j;
+#endif
+}
+// tree height of a table of E entries: its padded size is pow2_above(E) - 1
+__device__ __forceinline__ int wg_height(int E) { return 32 - __clz(E); }
 
 // AND / OR over the workgroup of a per-wave flag (each wave's lane 0 has
 // stored it in f[w] before a plain barrier): two 16-byte LDS reads, where
@@ -2132,6 +2158,22 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
   int xg[GK_WG_VPT];
   uint32_t slot[GK_WG_VPT];  // an unsorted value's member slot in its gap
   for (int pass = 0;; ++pass) {
+#if GK_WG_EYTZ
+    {
+      const int H = wg_height(E);
+#pragma unroll
+      for (int r = 0; r < GK_WG_VPT; ++r) xg[r] = 1;
+      for (int l = 0; l < H; ++l) {
+        double tt[GK_WG_VPT];
+#pragma unroll
+        for (int r = 0; r < GK_WG_VPT; ++r) tt[r] = tv[xg[r]];
+#pragma unroll
+        for (int r = 0; r < GK_WG_VPT; ++r) xg[r] = 2 * xg[r] + ((tt[r] <= xv[r]) ? 1 : 0);
+      }
+#pragma unroll
+      for (int r = 0; r < GK_WG_VPT; ++r) xg[r] = min(xg[r] - (1 << H), E);
+    }
+#else
 #pragma unroll
     for (int r = 0; r < GK_WG_VPT; ++r) xg[r] = 0;
     for (int step = gk_pow2_above(E) >> 1; step > 0; step >>= 1) {
@@ -2143,6 +2185,7 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
     }
 #pragma unroll
     for (int r = 0; r < GK_WG_VPT; ++r) xg[r] = min(xg[r], E);
+#endif
     if (pass > 0) {  // (the re-search of a sorted batch: counts start over)
       for (int j = t; j <= E; j += GK_WG_T) gpk[j] = 0u;
       __syncthreads();
@@ -2303,6 +2346,7 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
   const int newE = (int)(total & 0xffffu);
   if (newE > GK_WG_CAP - 1) return -1;  // (uniform: total comes from LDS) one slot stays free for the padding
   const int totm = (int)(total >> 16);
+  const int Ho = wg_height(E), Hn = wg_height(newE);  // the old / new table's tree heights
   if (sorted && !wg_flags_any(L.xcrowd)) {
     // ---- entry-side emit (sorted, no crowded thread): each thread stores its
     //      entries' gap survivors (sorted positions member base + absorbed ..
@@ -2323,7 +2367,7 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
         const int ob = (int)(base & 0xffffu);
         if (kk & GK_KEEP_BIT) {
           const int pos = ob + m - ka;
-          nv[pos] = tv[j];
+          nv[wg_slot(pos, Hn)] = tv[wg_slot(j, Ho)];
           ngd[pos] = make_int2(eG[k], ed[k]);
         }
         sb[k] = st_;
@@ -2355,7 +2399,7 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
 #pragma unroll
       for (int u = 0; u < GK_WG_EMIT_U; ++u) {
         if (o0 + u < st_) {
-          nv[dpos[u]] = xs[u];
+          nv[wg_slot(dpos[u], Hn)] = xs[u];
           ngd[dpos[u]] = make_int2(1, dd[u]);
         }
       }
@@ -2370,13 +2414,13 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
         const int rr = rk - qq * cs;
         if (rr == cs - 1 || rk == mEa - 1) {
           const int pos = obE + qq;
-          nv[pos] = xv[r];
+          nv[wg_slot(pos, Hn)] = xv[r];
           ngd[pos] = make_int2(rr + 1, 0);
         }
       }
     }
     const int hi = gk_pow2_above(newE) - 1;
-    for (int j = newE + t; j < hi; j += GK_WG_T) nv[j] = __longlong_as_double(0x7ff0000000000000LL);
+    for (int j = newE + t; j < hi; j += GK_WG_T) nv[wg_slot(j, Hn)] = __longlong_as_double(0x7ff0000000000000LL);
     GK_WMARK(11);
     __syncthreads();
     GK_WMARK(12);
@@ -2398,7 +2442,7 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
         L.gdel[j] = G + d - 1;
         if (kk & GK_KEEP_BIT) {
           const int pos = (int)(base & 0xffffu) + m - ka;
-          nv[pos] = tv[j];
+          nv[wg_slot(pos, Hn)] = tv[wg_slot(j, Ho)];
           ngd[pos] = make_int2(G, d);
         }
         base += ((uint32_t)m << 16) | (uint32_t)(m - ka + ((kk & GK_KEEP_BIT) ? 1 : 0));
@@ -2477,7 +2521,7 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
         const int k = L.gk[gap] & ~GK_KEEP_BIT;
         if (rk >= k) {
           const int pos = (int)(pk & 0xffffu) + rk - k;
-          nv[pos] = xv[r];
+          nv[wg_slot(pos, Hn)] = xv[r];
           ngd[pos] = make_int2(1, L.gdel[gap]);
         }
       } else {
@@ -2486,7 +2530,7 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
         const int rr = rk - qq * cs;
         if (rr == cs - 1 || rk == m - 1) {
           const int pos = (int)(pk & 0xffffu) + qq;
-          nv[pos] = xv[r];
+          nv[wg_slot(pos, Hn)] = xv[r];
           ngd[pos] = make_int2(rr + 1, 0);
         }
       }
@@ -2494,7 +2538,7 @@ __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG
   }
   // +inf padding for the next search, up to pow2_above(newE) - 2
   const int hi = gk_pow2_above(newE) - 1;
-  for (int j = newE + t; j < hi; j += GK_WG_T) nv[j] = __longlong_as_double(0x7ff0000000000000LL);
+  for (int j = newE + t; j < hi; j += GK_WG_T) nv[wg_slot(j, Hn)] = __longlong_as_double(0x7ff0000000000000LL);
   GK_WMARK(11);  // values: records read, survivors stored, padding
   __syncthreads();
   GK_WMARK(12);  // end barrier
@@ -2541,10 +2585,25 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
   if (go) {
     // launched ahead of k_long_prep (the stream list, the presort plan and
     // this launch's stream count): wait for its word, then every thread
-    // acquires it (the list was written on another CU)
-    if (t == 0)
-      while (__hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) __builtin_amdgcn_s_sleep(8);
+    // acquires it (the list was written on another CU).  Bounded: if the word
+    // does not come within GK_WG_GO_TICKS (kernels serialised -- a profiler's
+    // counter passes, AMD_SERIALIZE_KERNEL -- or no CU left for k_long_prep)
+    // the workgroup leaves without taking a stream, and the launch the call
+    // enqueues behind k_long_prep (gk_capi.cpp stats_fork) takes them all.
+    if (t == 0) {
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      int ok = 1;
+      while (__hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > GK_WG_GO_TICKS) {
+          ok = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(8);
+      }
+      L.go_ok = ok;
+    }
     __syncthreads();
+    if (!L.go_ok) return;  // (workgroup-uniform)
     (void)__hip_atomic_load(go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
   }
   const int64_t K = *wg_count;
@@ -2580,13 +2639,14 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
     bool ok = E <= GK_WG_CAP - 1 && P <= GK_WG_PMAX && gk_count_ok(st, n + (Lx > 0 ? Lx : 0));
     int cur = 0;
     if (ok) {
+      const int H = wg_height(E);
       for (int j = t; j < E; j += GK_WG_T) {
         const GKRec rc = tab[j];
-        L.tv[0][j] = rc.v;
+        L.tv[0][wg_slot(j, H)] = rc.v;
         L.tgd[0][j] = make_int2(rc.g, rc.d);
       }
       const int hi = gk_pow2_above(E) - 1;
-      for (int j = E + t; j < hi; j += GK_WG_T) L.tv[0][j] = __longlong_as_double(0x7ff0000000000000LL);
+      for (int j = E + t; j < hi; j += GK_WG_T) L.tv[0][wg_slot(j, H)] = __longlong_as_double(0x7ff0000000000000LL);
       for (int j = t; j <= GK_WG_CAP; j += GK_WG_T) L.gpk[0][j] = 0u;  // (flush_wg zeroes the other)
     }
     __syncthreads();
@@ -2714,9 +2774,10 @@ __global__ __launch_bounds__(GK_WG_T) void k_ingest_wg(GKState st, const double*
       __syncthreads();
       continue;
     }
+    const int Hw = wg_height(E);
     for (int j = t; j < E; j += GK_WG_T) {
       GKRec rc;
-      rc.v = L.tv[cur][j];
+      rc.v = L.tv[cur][wg_slot(j, Hw)];
       const int2 gd = L.tgd[cur][j];
       rc.g = gd.x;
       rc.d = gd.y;

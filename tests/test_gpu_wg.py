@@ -117,3 +117,47 @@ def test_wg_plain_ingest_then_query(gpu_device, monkeypatch, capfd):
     assert took and max(took) > 0
     assert_same_quantiles(ss.quantiles(QS).cpu().numpy(), o.quantiles(QS), "final query", small_of(o, EPS))
     assert_same_state(ss, o, "after query")
+
+
+SERIAL_SCRIPT = r'''
+import sys, numpy as np, torch
+sys.path[:0] = sys.argv[1].split(":")
+from gk_oracle_c import OracleSet
+from parity_util import _ss, assert_same_state
+dev = torch.device("cuda", 0)
+rng = np.random.default_rng(41)
+lens = rng.integers(0, 3000, 40)
+lens[:3] = [600_000, 450_123, 400_000]
+ss = _ss(40, 0.001, dev)
+o = OracleSet(40, 0.001)
+for call in range(2):
+    seqs = [rng.lognormal(0, 1, int(L)) for L in lens]
+    offs = np.zeros(41, np.int64)
+    offs[1:] = np.cumsum(lens)
+    flat = np.concatenate(seqs)
+    ss.ingest(torch.from_numpy(flat).to(dev), torch.from_numpy(offs).to(dev))
+    o.ingest(flat, offs)
+assert_same_state(ss, o, "serialised kernels")
+print("OK")
+'''
+
+
+def test_wg_early_launch_survives_serialised_kernels(gpu_device, tmp_path):
+    """ADVICE r05: the early k_ingest_wg grid spins on the device for
+    k_long_prep's word.  With every kernel serialised (AMD_SERIALIZE_KERNEL=3,
+    as under a profiler's counter passes) k_long_prep cannot run beside it:
+    the spin is bounded (1 s), the workgroups leave without a stream, and the
+    launch the call enqueues behind k_long_prep takes them -- no hang, the
+    same bits as the oracle."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    paths = ":".join([os.path.join(root, "sketches-py_amd"), os.path.join(root, "oracle"),
+                      os.path.join(root, "tests")])
+    env = dict(os.environ, AMD_SERIALIZE_KERNEL="3", GK_WG="1", GK_WG_EARLY="1", GK_WG_TRACE="1")
+    r = subprocess.run([sys.executable, "-c", SERIAL_SCRIPT, paths], capture_output=True, text=True, timeout=240,
+                       env=env)
+    assert r.returncode == 0 and "OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
+    took = [int(m) for m in re.findall(r"k_ingest_wg: (\d+) stream", r.stderr)]
+    assert took and max(took) > 0, r.stderr[-2000:]
