@@ -402,7 +402,7 @@ def main():
         gsync()
         warm_info["steps"], warm_info["seconds"] = nw, time.perf_counter() - tw
         for t_ss in timed_sets:
-            t_ss.timing(True)
+            t_ss.timing(True, stats=os.environ.get("GK_BENCH_STATS_TIMING") == "1")
             t_ss.read_timing()
         barrier()
         gsync()
@@ -573,7 +573,8 @@ def main():
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
                      "traffic_ratio": ratio, "traffic_source": traffic_src,
                      "bytes_per_launch": bytes_per_launch, "launch_ms": k_ms,
-                     "stats_kernel_ms": stats_ms / max(launches, 1)},
+                     "stats_kernel_ms": (stats_ms / max(launches, 1)
+                                         if os.environ.get("GK_BENCH_STATS_TIMING") == "1" else None)},
         "library": _library_identity(),
     }
     if per_rank is not None:

@@ -221,9 +221,11 @@ int64_t gk_num_promoted(const gk_set* set);   /* streams in the large class */
  * the set's host worker.  Diagnostics only: results never depend on it. */
 int64_t gk_host_chains_taken(gk_set* set);
 
-/* Kernel timing: when enabled, gk_ingest records HIP events around the flush
- * kernel it launches on `stream`; gk_timing_read returns the summed
- * milliseconds and the number of launches since the last read. */
+/* Kernel timing: `on` bit 0 -- gk_ingest records HIP events around the
+ * flush kernel it launches on `stream`; bit 1 -- also around the call's
+ * stats fork (stats_ms; two more event markers per call).  gk_timing_read
+ * returns the summed milliseconds and the number of launches since the last
+ * read. */
 int gk_timing_enable(gk_set* set, int on);
 int gk_timing_read(gk_set* set, double* flush_ms, double* stats_ms,
                    int64_t* launches);

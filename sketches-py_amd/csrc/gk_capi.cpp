@@ -104,6 +104,11 @@ struct gk_set {
   // a gk_reset came after the call whose counters are still in flight: its
   // deferred streams are void (every stream was reset; nothing to re-run)
   bool void_defer = false;
+  // the per-call counter block is known zero: gk_reset's k_reset zeroed it and
+  // nothing has written it since (begin_call then skips its memset; cleared by
+  // begin_call and by the paths that write the block without it: run_merge,
+  // gk_import)
+  bool ctr_clean = false;
   int32_t fatal_seen = 0;  // device FATAL count already reported
   int sticky = GK_OK;      // asynchronous error reported by the next call / gk_sync
   std::string sticky_msg;
@@ -158,6 +163,9 @@ struct gk_set {
   const double* hc_x = nullptr;     // the call's values and offsets
   const int64_t* hc_offs = nullptr;
   bool forked = false;              // stats_fork launched on aux; stats_join / stats_abort joins it
+  bool sl_inline = false;           // no fork: stats_join launches k_stats_long on the call's stream
+  const double* sl_x = nullptr;     // (its arguments)
+  const int64_t* sl_offs = nullptr;
   // one copy stream for every host thread's chunk copies, made at the first
   // host-walked chain (the box runs 4 hardware queues per process: a copy
   // stream sharing the ingest's or aux's queue waits behind their kernels --
@@ -198,7 +206,8 @@ struct gk_set {
   int hc_last_rc = GK_OK;
   std::string hc_last_msg;
   // timing: event pairs recorded around the timed launches, summed at read
-  bool timing = false;
+  bool timing = false;        // events around the class-0 ingest launch (gk_timing_enable bit 0)
+  bool timing_stats = false;  // and around stats_fork's launches (bit 1: two more markers per call)
   std::vector<hipEvent_t> tev_flush, tev_stats;
   size_t n_flush = 0, n_stats = 0;
 };
@@ -316,7 +325,9 @@ int mark_done(gk_set* h, hipStream_t s);
 // (deferred / long-stream counts, re-run and overflow list lengths, the
 // launches' stream hand-out counters; gk_launch.h GK_CTR_*).
 int begin_call(gk_set* h, hipStream_t s) {
-  HIP_TRY(hipMemsetAsync(h->d_ctr + GK_CTR_CALL, 0, GK_CALL_BYTES - GK_CTR_CALL * sizeof(int32_t), s));
+  if (!h->ctr_clean)
+    HIP_TRY(hipMemsetAsync(h->d_ctr + GK_CTR_CALL, 0, GK_CALL_BYTES - GK_CTR_CALL * sizeof(int32_t), s));
+  h->ctr_clean = false;
   h->next_work = 0;
   return GK_OK;
 }
@@ -700,6 +711,9 @@ void stats_abort(gk_set* h, hipStream_t s) {
   if (h->wg_early) (void)hipStreamWaitEvent(s, h->ev_wg, 0);  // (launched by stats_fork: joined here too)
   h->wg_early = false;
   if (h->forked) (void)hipStreamWaitEvent(s, h->ev_join, 0);
+  if (h->sl_inline)
+    (void)gk_launch_stats_long(h->st, h->sl_x, h->sl_offs, h->d_long_list, nullptr, h->d_long_count, nullptr, s);
+  h->sl_inline = false;
   if (h->presort_active) (void)hipStreamWaitEvent(s, h->ev_presort, 0);
   h->presort_active = false;
   if (h->hc_active) {
@@ -714,7 +728,7 @@ void stats_abort(gk_set* h, hipStream_t s) {
 }
 
 int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s, int force) {
-  hipEvent_t t0 = h->timing ? timing_event(h->tev_stats, h->n_stats) : nullptr;
+  hipEvent_t t0 = h->timing_stats ? timing_event(h->tev_stats, h->n_stats) : nullptr;
   if (t0) HIP_TRY(hipEventRecord(t0, s));
   // k_ingest_wg ahead of everything else of the call (GK_WG_EARLY, default
   // 1): launched behind the call's counter reset only, its workgroups take
@@ -786,7 +800,23 @@ int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s, i
     h->hc_x = x;
     h->hc_offs = offs;
   }
-  HIP_TRY(hipEventRecord(h->ev_fork, s));
+  const bool presort = h->ps.list_ws && h->ps.ws && h->ps.ws_cap > 0;
+  // No fork when nothing but k_stats_long would go to the aux streams and the
+  // set's last completed call listed no long stream (its counter words come
+  // back with every call): k_stats_long then runs on `s` behind the ingest
+  // (stats_join).  Forked, its workgroups must reach the CUs before the
+  // persistent ingest grid -- the fork's cross-queue wake-up (~13 us) is then
+  // on the step's critical path, and a k_stats_long dispatched beside the
+  // ingest grid cost the cfg3 launch 8 % (profiles/r06/r06q_*).  A wrong
+  // guess costs time only: the walk is the same on either stream.
+  h->sl_inline = stats_fused(h) && !prep && !early && !hc_on && !presort && !h->aux2 && h->h_ctr &&
+                 h->h_ctr[GK_CTR_LONG] == 0 && !getenv("GK_SL_FORK");
+  if (h->sl_inline) {
+    h->sl_x = x;
+    h->sl_offs = offs;
+  } else {
+    HIP_TRY(hipEventRecord(h->ev_fork, s));
+  }
   if (wwork_early) {
     // behind k_long_prep, on the same hand-out counter: the streams of any
     // early workgroup that gave up waiting for k_long_prep's word (bounded
@@ -797,13 +827,14 @@ int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s, i
                                 ovf_list(h, 0), wwork_early, h->ps, h->aux2, nullptr));
     HIP_TRY(hipEventRecord(h->ev_wg, h->aux2));
   }
-  HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_fork, 0));
-  h->forked = true;
-  HIP_TRY(gk_launch_stats_long(h->st, x, offs, h->d_long_list, prep ? h->d_long_n : nullptr, h->d_long_count,
-                               hc_on ? h->d_hc_count : nullptr, h->aux));
-  h->hc_active = hc_on;  // (stats_join hands the picked chains to the worker)
-  HIP_TRY(hipEventRecord(h->ev_join, h->aux));
-  const bool presort = h->ps.list_ws && h->ps.ws && h->ps.ws_cap > 0;
+  if (!h->sl_inline) {
+    HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_fork, 0));
+    h->forked = true;
+    HIP_TRY(gk_launch_stats_long(h->st, x, offs, h->d_long_list, prep ? h->d_long_n : nullptr, h->d_long_count,
+                                 hc_on ? h->d_hc_count : nullptr, h->aux));
+    h->hc_active = hc_on;  // (stats_join hands the picked chains to the worker)
+    HIP_TRY(hipEventRecord(h->ev_join, h->aux));
+  }
   if (presort) {
     // with k_ingest_wg beside it (ps.done): on its own stream, joined by
     // stats_join; else on aux2 ahead of k_ingest_wg
@@ -819,7 +850,7 @@ int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s, i
   // on aux2)
   if (presort && !h->ps.wg_count) HIP_TRY(hipStreamWaitEvent(s, h->ev_presort, 0));
   if (h->ps.ws_need) HIP_TRY(hipMemcpyAsync(h->h_ws_need, h->ps.ws_need, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  hipEvent_t t1 = h->timing ? timing_event(h->tev_stats, h->n_stats) : nullptr;
+  hipEvent_t t1 = h->timing_stats ? timing_event(h->tev_stats, h->n_stats) : nullptr;
   if (t1) HIP_TRY(hipEventRecord(t1, s));
   return GK_OK;
 }
@@ -829,8 +860,13 @@ int stats_join(gk_set* h, hipStream_t s, const GKQuery& q) {
     h->wg_early = false;
     HIP_TRY(hipStreamWaitEvent(s, h->ev_wg, 0));
   }
+  if (h->sl_inline) {
+    h->sl_inline = false;
+    HIP_TRY(gk_launch_stats_long(h->st, h->sl_x, h->sl_offs, h->d_long_list, nullptr, h->d_long_count, nullptr, s));
+  } else {
+    HIP_TRY(hipStreamWaitEvent(s, h->ev_join, 0));
+  }
   h->forked = false;
-  HIP_TRY(hipStreamWaitEvent(s, h->ev_join, 0));
   if (h->presort_active) {
     h->presort_active = false;
     HIP_TRY(hipStreamWaitEvent(s, h->ev_presort, 0));
@@ -965,6 +1001,7 @@ int run_merge(gk_set* dst, const MergeArgsHost& base, hipStream_t s) {
   MergeArgsHost a = base;
   const GKPoolDev pool = pool_args(dst);
   int64_t todo = 0;
+  dst->ctr_clean = false;
   HIP_TRY(hipMemsetAsync(dst->d_ovfc, 0, kRounds * sizeof(int32_t), s));
   for (int level = 0; level < dst->st.nclass; ++level) {
     const int cap = dst->st.cap[level];
@@ -1290,8 +1327,11 @@ int gk_reset(gk_set* h, void* stream) {
   // (k_reset puts every stream back in class 0: cls = slot = 0)
   // slots, member lists and re-run lists start over (FATAL stays cumulative:
   // a readback still in flight carries it)
-  HIP_TRY(gk_launch_reset(h->st, s, h->d_ctr));  // (+ counter words [0, GK_CTR_FATAL): no separate memset)
+  // (+ counter words [0, GK_CTR_FATAL) and the per-call block: no separate
+  // memset, and none at the next call's begin_call)
+  HIP_TRY(gk_launch_reset(h->st, s, h->d_ctr));
   h->no_members = true;
+  h->ctr_clean = true;
   return GK_OK;
 }
 
@@ -1572,6 +1612,7 @@ int gk_import(gk_set* h, const int64_t* offs, const double* v, const int32_t* g,
   if (S == 0) return GK_OK;
   rc = gk_sync(h, stream);
   if (rc) return rc;
+  h->ctr_clean = false;  // (writes words of the per-call block below)
   {
     int32_t* bad = h->d_ctr + GK_CTR_BADPEND;
     HIP_TRY(hipMemsetAsync(bad, 0, sizeof(int32_t), s));
@@ -1877,7 +1918,8 @@ int64_t gk_num_promoted(const gk_set* h) {
 int gk_timing_enable(gk_set* h, int on) {
   int rc = check_set(h);
   if (rc) return rc;
-  h->timing = on != 0;
+  h->timing = (on & 1) != 0;
+  h->timing_stats = (on & 2) != 0;
   return GK_OK;
 }
 

@@ -4211,6 +4211,9 @@ __device__ __attribute__((noinline)) double small_quantiles(SmallLDS<VPL>& L, in
 #ifndef GK_FS_LAG_DEFAULT
 #define GK_FS_LAG_DEFAULT 256  // streams the ingest hand-out runs ahead of a stats batch (GK_FS_LAG overrides)
 #endif
+#ifndef GK_FS_DRAIN
+#define GK_FS_DRAIN 1  // ingest waves walk their part's unclaimed stats batches once its streams run out
+#endif
 #ifndef GK_FS_SPIN_MAX
 #define GK_FS_SPIN_MAX (1 << 16)  // pacing waits at most this many s_sleeps per batch (no deadlock by construction)
 #endif
@@ -4609,6 +4612,12 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
     prof_done_any = true;
 #endif
   }
+  // The part's streams have run out: its stats batches still unclaimed are
+  // walked by every wave of the part as it gets here, not by the stats waves
+  // alone (which trail the hand-out: until round 6 they ended the launch up
+  // to ~200 us after the last ingest wave).  The part's hand-out is past its
+  // end, so the pacing never waits here.
+  if (FS && GK_FS_DRAIN) fused_stats_role(st, x, offs, work, part, nparts, count, fs_pace, fs_lag, lane);
 #ifdef GK_PROF
   if (lane == 0)
     for (int i = 0; i < GK_PROF_NSEC; ++i) atomicAdd(&gk_prof_acc[i], L.prof[i]);
@@ -5016,7 +5025,9 @@ __global__ __launch_bounds__(64) void k_merge(MergeArgs a) {
 // (words [0, GK_CTR_FATAL); FATAL stays cumulative)
 __global__ void k_reset(GKState st, int32_t* __restrict__ ctr) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (ctr && s < GK_CTR_FATAL) ctr[s] = 0;
+  // (+ the per-call block [GK_CTR_CALL, GK_CALL_BYTES): the next call's
+  // begin_call then skips its memset -- one dispatch fewer per step)
+  if (ctr && (s < GK_CTR_FATAL || (s >= GK_CTR_CALL && s < GK_CALL_BYTES / 4))) ctr[s] = 0;
   if (s >= st.S) return;
   st.n[s] = 0;
   st.E[s] = 0;
@@ -5533,7 +5544,7 @@ hipError_t gk_launch_rtab(const GKState& st, hipStream_t stream) {
 
 hipError_t gk_launch_reset(const GKState& st, hipStream_t stream, int32_t* ctr) {
   if (st.S <= 0 && !ctr) return hipSuccess;
-  const int64_t grid = (std::max<int64_t>(st.S, GK_CTR_FATAL) + 255) / 256;
+  const int64_t grid = (std::max<int64_t>(st.S, GK_CALL_BYTES / 4) + 255) / 256;
   hipLaunchKernelGGL(k_reset, dim3((unsigned)grid), dim3(256), 0, stream, st, ctr);
   return hipGetLastError();
 }

@@ -154,7 +154,8 @@ hipError_t gk_launch_query_list(const GKState& st, const int32_t* list, const in
 size_t gk_merge_lds_bytes(int cap, int pmax);
 hipError_t gk_launch_merge(const MergeArgsHost& h, hipStream_t stream);
 // every stream back to an empty sketch in class 0; ctr: also zero the set's
-// counter words [0, GK_CTR_FATAL) (slots used, member-list lengths)
+// counter words [0, GK_CTR_FATAL) (slots used, member-list lengths) and the
+// per-call block [GK_CTR_CALL, GK_CALL_BYTES) (what begin_call's memset zeroes)
 hipError_t gk_launch_reset(const GKState& st, hipStream_t stream, int32_t* ctr = nullptr);
 // fills st.rtab (reciprocals 1.0/k, k < st.rtab_n)
 hipError_t gk_launch_rtab(const GKState& st, hipStream_t stream);

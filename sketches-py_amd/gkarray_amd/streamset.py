@@ -441,8 +441,10 @@ class StreamSet:
                                                 _ptr(t_o), self._sp()))
 
     # ------------------------------------------------------------------ timing
-    def timing(self, on=True):
-        self._check(self._lib.gk_timing_enable(self._h, 1 if on else 0))
+    def timing(self, on=True, stats=False):
+        """HIP events around the ingest launch (and, stats=True, around the
+        call's stats fork: two more event markers per call)."""
+        self._check(self._lib.gk_timing_enable(self._h, (1 | (2 if stats else 0)) if on else 0))
 
     def read_timing(self):
         f = ctypes.c_double()
