@@ -17,6 +17,7 @@
 //                           the incoming list, general four-rule walk (gk:76-106)
 //   k_export / k_import / k_reset: state movement
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <math.h>
 
@@ -4228,9 +4229,9 @@ __device__ __attribute__((noinline)) double small_quantiles(SmallLDS<VPL>& L, in
 template <int DEPTH = GK_FS_DEPTH>
 __device__ __forceinline__ void fused_stats_role(const GKState& st, const double* __restrict__ x,
                                                  const int64_t* __restrict__ offs,
-                                                 unsigned long long* __restrict__ work, int part, int nparts,
+                                                 unsigned long long* __restrict__ work, int part, int lgp,
                                                  int64_t count, int pace, int lag, int lane) {
-  const int64_t pbeg = count * part / nparts, pend = count * (part + 1) / nparts;
+  const int64_t pbeg = (count * part) >> lgp, pend = (count * (part + 1)) >> lgp;
   const int64_t nb = (pend - pbeg + 63) / 64;
   unsigned long long* __restrict__ swork = work + GK_SWORK_IDX + 16 * part;
   unsigned long long* __restrict__ iwork = work + 16 * part;  // the part's ingest hand-out counter
@@ -4251,7 +4252,9 @@ __device__ __forceinline__ void fused_stats_role(const GKState& st, const double
         __builtin_amdgcn_s_sleep(8);
       }
     }
-    const int64_t s = pbeg + b * 64 + lane;
+    // (stream ids fit in 32 bits; a 64-bit pbeg + lane hoisted out of the
+    // batch loop was the launch's one remaining scratch spill)
+    const int64_t s = (int64_t)((int)(pbeg + b * 64) + lane);
     const bool live = s < pend;
     const int64_t xo = live ? offs[s] : 0;
     int64_t rem = live ? offs[s + 1] - xo : 0;
@@ -4379,19 +4382,26 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
 #ifndef GK_WORK_CHUNK
 #define GK_WORK_CHUNK 2  // streams per grab
 #endif
-  const int nparts = (int)min((unsigned)GK_WORK_PARTS, gridDim.x);  // every part has a wave
-  const int part = (int)(blockIdx.x % (unsigned)nparts);
+  // parts: a power of two, at most GK_WORK_PARTS and the grid (every part
+  // has a wave), so that the part bounds are scalar shifts (a 64-bit division
+  // here was VALU code whose results the flush loop's register pressure
+  // spilled to scratch -- and a launch with scratch costs the step two
+  // dispatch gaps of ~5 us)
+  static_assert((GK_WORK_PARTS & (GK_WORK_PARTS - 1)) == 0, "a power of two");
+  int lgp = 0;
+  while ((2 << lgp) <= GK_WORK_PARTS && (2u << lgp) <= gridDim.x) ++lgp;
+  const int part = (int)(blockIdx.x & ((1u << lgp) - 1u));
 #ifdef GK_TIMELINE
   if (lane == 0 && blockIdx.x < GK_TL_MAXW) {
     gk_tl_wave[5 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     gk_tl_wave[5 * blockIdx.x + 3] = __builtin_amdgcn_s_memtime();
   }
 #endif
-  if (FS && (int)blockIdx.x < nstat) fused_stats_role(st, x, offs, work, part, nparts, count, fs_pace, fs_lag, lane);
+  if (FS && (int)blockIdx.x < nstat) fused_stats_role(st, x, offs, work, part, lgp, count, fs_pace, fs_lag, lane);
 #ifdef GK_TIMELINE
   if (lane == 0 && blockIdx.x < GK_TL_MAXW) gk_tl_wave[5 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
 #endif
-  const int64_t pbeg = count * part / nparts, pend = count * (part + 1) / nparts;
+  const int64_t pbeg = (count * part) >> lgp, pend = (count * (part + 1)) >> lgp;
   // the query's q values, the same for every stream: lane l holds q l
   const double qpre = (qs && lane < nq) ? qs[lane] : 0.0;
   int64_t cur = 0, cend = 0;
@@ -4597,9 +4607,13 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
     }
     if (qs) {
       for (int q0 = 0; q0 < nq; q0 += 64) {
-        const double qv = nq <= 64 ? qpre : ((q0 + lane < nq) ? qs[q0 + lane] : 0.0);
+        // (the lane made opaque per chunk: its 64-bit address math is not
+        // hoisted out of the stream loop, where it was spilled to scratch)
+        int ql = lane;
+        __asm__ volatile("" : "+v"(ql));
+        const double qv = nq <= 64 ? qpre : ((q0 + ql < nq) ? qs[q0 + ql] : 0.0);
         const double r = small_quantiles<VPL>(L, E, n, smn, smx, st.inv_eps, st.eps, qv, min(nq - q0, 64), qmode, lane);
-        if (q0 + lane < nq) qout[s * (int64_t)nq + q0 + lane] = r;
+        if (q0 + ql < nq) qout[s * (int64_t)nq + q0 + ql] = r;
       }
     }
     write_back();
@@ -4617,7 +4631,7 @@ __global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st,
   // alone (which trail the hand-out: until round 6 they ended the launch up
   // to ~200 us after the last ingest wave).  The part's hand-out is past its
   // end, so the pacing never waits here.
-  if (FS && GK_FS_DRAIN) fused_stats_role(st, x, offs, work, part, nparts, count, fs_pace, fs_lag, lane);
+  if (FS && GK_FS_DRAIN) fused_stats_role(st, x, offs, work, part, lgp, count, fs_pace, fs_lag, lane);
 #ifdef GK_PROF
   if (lane == 0)
     for (int i = 0; i < GK_PROF_NSEC; ++i) atomicAdd(&gk_prof_acc[i], L.prof[i]);
@@ -5289,7 +5303,7 @@ template <int VPL>
 static hipError_t launch_ingest_small(const GKState& st, const double* x, const int64_t* offs, const int32_t* list,
                                       int64_t count, int force, int32_t* ovf_count, int32_t* ovf_list,
                                       const GKQuery& q, unsigned long long* work, int fused_stats,
-                                      hipStream_t stream) {
+                                      hipStream_t stream, hipEvent_t ev0, hipEvent_t ev1) {
   if (count <= 0) return hipSuccess;
   if (!work) return hipErrorInvalidValue;
   static std::atomic<int> occ_cache[GK_MAX_DEV];  // (queried once per device)
@@ -5313,12 +5327,14 @@ static hipError_t launch_ingest_small(const GKState& st, const double* x, const 
   const int pace = nstat > 0 && grid >= 4 * (int64_t)nstat && grid >= 8 * GK_WORK_PARTS ? 1 : 0;
   static const int lag = getenv("GK_FS_LAG") ? atoi(getenv("GK_FS_LAG")) : GK_FS_LAG_DEFAULT;
   if (list) return hipErrorInvalidValue;  // class 0 over every stream only
+  // (ev0 / ev1: recorded by the dispatch itself -- the kernel's own start and
+  // end -- when given)
   if (nstat > 0)
-    hipLaunchKernelGGL((k_ingest_small<VPL, true>), dim3((unsigned)grid), dim3(64), 0, stream, st, x, offs, count,
-                       force, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode, work, nstat, pace, lag);
+    hipExtLaunchKernelGGL((k_ingest_small<VPL, true>), dim3((unsigned)grid), dim3(64), 0, stream, ev0, ev1, 0, st, x,
+                          offs, count, force, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode, work, nstat, pace, lag);
   else
-    hipLaunchKernelGGL((k_ingest_small<VPL, false>), dim3((unsigned)grid), dim3(64), 0, stream, st, x, offs, count,
-                       force, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode, work, nstat, pace, lag);
+    hipExtLaunchKernelGGL((k_ingest_small<VPL, false>), dim3((unsigned)grid), dim3(64), 0, stream, ev0, ev1, 0, st, x,
+                          offs, count, force, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode, work, nstat, pace, lag);
   return hipGetLastError();
 }
 
@@ -5346,14 +5362,16 @@ hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x
                             int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list, const GKQuery& q,
                             unsigned long long* work, const int32_t* prio, const int32_t* prio_count,
                             const double* psort, const int64_t* prio_ws, const int32_t* prio_skip, int fused_stats,
-                            hipStream_t stream) {
+                            hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop) {
   switch (cap) {
     case SMALL_CAP:
       if (list || count_ptr || lcls != 0) return hipErrorInvalidValue;  // class 0 over every stream only
       if (vpl == 1)
-        return launch_ingest_small<1>(st, x, offs, list, count, force, ovf_count, ovf_list, q, work, fused_stats, stream);
+        return launch_ingest_small<1>(st, x, offs, list, count, force, ovf_count, ovf_list, q, work, fused_stats, stream,
+                                      ev_start, ev_stop);
       if (vpl == 2)
-        return launch_ingest_small<2>(st, x, offs, list, count, force, ovf_count, ovf_list, q, work, fused_stats, stream);
+        return launch_ingest_small<2>(st, x, offs, list, count, force, ovf_count, ovf_list, q, work, fused_stats, stream,
+                                      ev_start, ev_stop);
       return hipErrorInvalidValue;
     case 2048:
       return launch_ingest_vpl<2048>(vpl, st, x, offs, list, count, count_ptr, lcls, force, cap, nullptr, 0, 0,
