@@ -214,6 +214,22 @@ struct gk_set {
 
 namespace {
 
+// Every launch of the last class counts the streams that outgrow it as fatal
+// itself (k_ingest pmode bit 1), so no promotion round is needed past it --
+// unless that class runs k_ingest_big (or there is a single class).
+bool fatal_direct(const gk_set* h) { return h->st.nclass >= 2 && !h->big[h->st.nclass - 1]; }
+
+// What a launch of class c >= 1 (k_ingest) does itself with the streams that
+// outgrow it, instead of listing them for the next promotion round: 2 =
+// count them fatal (the last class), 4 = defer them (the next class has no
+// slot during this call: the round would defer every one), 0 = list them.
+int overflow_direct(const gk_set* h, int c) {
+  const int R = h->st.nclass;
+  if (c < 1 || c >= R || h->big[c]) return 0;
+  if (c == R - 1) return fatal_direct(h) ? 2 : 0;
+  return h->st.alloc[c + 1] == 0 ? 4 : 0;
+}
+
 GKPoolDev pool_args(const gk_set* h) {
   GKPoolDev p;
   p.ctr = h->d_ctr;
@@ -506,10 +522,12 @@ bool stats_fused(const gk_set* h);
 // whose length is *count_ptr (device).  Overflowing streams go to round r's list.
 hipError_t launch_class(gk_set* h, int c, const double* x, const int64_t* offs, const int32_t* list,
                         const int32_t* count_ptr, int r, int force, const GKQuery& q, hipStream_t stream,
-                        bool prio = false, bool wg = false, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
+                        bool prio = false, bool wg = false, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr,
+                        int pmode = 0) {
   if (c > 0 && h->st.alloc[c] == 0) return hipSuccess;  // no slot yet: no member
   unsigned long long* work = work_counter(h, c == 0 && h->st.cap[0] == GK_SMALL_CAP && !h->big[0]);
   if (!work) return hipErrorInvalidValue;
+  const GKPoolDev pool = pool_args(h);
   if (h->big[c])
     return gk_launch_ingest_big(h->st.cap[c], h->st, x, offs, list, list ? 0 : h->S, count_ptr, c, force,
                                 h->d_ws[c], h->ws_bytes[c], h->ws_blocks[c], ovf_count(h, r), ovf_list(h, r), q,
@@ -519,7 +537,8 @@ hipError_t launch_class(gk_set* h, int c, const double* x, const int64_t* offs, 
                           prio ? h->d_long_list : nullptr, prio ? h->d_long_count : nullptr,
                           prio && h->ps.ws ? h->ps.ws : nullptr, prio && h->ps.ws ? h->ps.list_ws : nullptr,
                           prio && wg ? h->ps.wg_count : nullptr,
-                          (prio && c == 0 && stats_fused(h)) ? h->fused_stats : 0, stream, ev0, ev1);
+                          (prio && c == 0 && stats_fused(h)) ? h->fused_stats : 0, stream, ev0, ev1, &pool,
+                          pmode | overflow_direct(h, c));
 }
 
 // gk:52-59 for a batch: k_stats over every stream on `s` (it lists the
@@ -924,9 +943,36 @@ int promote_rounds(gk_set* h, const double* x, const int64_t* offs, int force, c
     // (fresh: round r-1 re-ran class r-1 only; a class with no slots has no
     // launch, and then round r has nothing to promote)
     if (fresh && !ran) break;
+    // (past the last class only fatal streams are left to count, and with
+    // fatal_direct its launches counted them; fresh: round r-1 re-ran class
+    // r-1 only, which counted or deferred its overflows itself)
+    if (r == R && fatal_direct(h)) break;
+    if (fresh && overflow_direct(h, r - 1)) break;
     int32_t* rcnt = h->d_ctr + GK_CTR_RCNT + GK_MAX_CLASSES * r;  // zeroed at the start of the call
     pool.rcnt = rcnt;
     h->no_members = false;
+    // Fused round: every class launched this round has slots and runs
+    // k_ingest, so each launch promotes the streams of round r-1's overflow
+    // list whose next class is its own (k_ingest pmode bit 0) -- no
+    // k_promote_dev launch and no re-run list.  GK_PROMOTE_FUSE=0: always the
+    // separate promotion.
+    const int c_end = fresh ? std::min(r + 1, R) : R;
+    static const bool fuse_env = !getenv("GK_PROMOTE_FUSE") || atoi(getenv("GK_PROMOTE_FUSE")) != 0;
+    bool fuse = fuse_env && r < R;
+    for (int c = r; c < c_end; ++c) fuse = fuse && h->st.alloc[c] > 0 && !h->big[c];
+    if (fuse) {
+      ran = false;
+      for (int c = r; c < c_end; ++c) {
+        ran = true;
+        HIP_TRY(launch_class(h, c, x, offs, ovf_list(h, r - 1), ovf_count(h, r - 1), r, force, q, stream, false, false,
+                             nullptr, nullptr, 1));
+        if (g_trace) {
+          HIP_TRY(hipStreamSynchronize(stream));
+          GK_TR("round %d: class %d promoted + re-run (fused)", r, c);
+        }
+      }
+      continue;
+    }
     HIP_TRY(gk_launch_promote_dev(h->st, ovf_count(h, r - 1), ovf_list(h, r - 1), -1, pool, stream));
     if (g_trace) {
       HIP_TRY(hipStreamSynchronize(stream));

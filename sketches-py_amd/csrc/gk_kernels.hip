@@ -1711,7 +1711,14 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
                                                const int32_t* __restrict__ prio_count,
                                                const double* __restrict__ psort,
                                                const int64_t* __restrict__ prio_ws,
-                                               const int32_t* __restrict__ prio_skip) {
+                                               const int32_t* __restrict__ prio_skip, GKPoolDev pool, int pmode) {
+  // pmode (promotion rounds, gk_capi.cpp promote_rounds): bit 0 -- `list` is
+  // the previous round's overflow list and this launch moves each stream
+  // whose next class is lcls into it first (k_promote_dev's level -1 step,
+  // one launch fewer per round); bit 1 -- lcls is the last class: a stream
+  // that outgrows it is counted fatal here instead of listed for a promotion
+  // round that could only count it; bit 2 -- the next class has no slot: a
+  // stream that outgrows lcls is deferred here (what that round would do)
   // the first *prio_skip streams of `prio` are k_ingest_wg's: skipped here,
   // and as many blocks leave at once so that its workgroups find free CUs
   const int skip = prio_skip ? *prio_skip : 0;
@@ -1776,7 +1783,37 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
     const double smx = __longlong_as_double(rfl64(__double_as_longlong(hv.mx)));
     if (wn < total) gk_hdr_issue(hv, st, offs, sid(wn));
     w = wn;
-    if (scls != lcls) continue;  // in another class: handled by that class's launch
+    int32_t ucls = scls, uslot = sslot;  // the stream's class and slot from here on
+    if (pmode & 1) {
+      if (scls + 1 != lcls) continue;  // another class's launch promotes it
+      int slot = -1;
+      if (lane == 0) {
+        slot = atomicAdd(&pool.ctr[GK_CTR_USED + lcls], 1);
+        if (slot >= st.alloc[lcls]) {
+          atomicSub(&pool.ctr[GK_CTR_USED + lcls], 1);
+          slot = -1;
+          pool.defer[atomicAdd(&pool.ctr[GK_CTR_DEFER], 1)] = (int32_t)s;  // (re-run by the host)
+        }
+      }
+      slot = __builtin_amdgcn_readfirstlane(__shfl(slot, 0, 64));
+      if (slot < 0) continue;
+      // the pre-call table moves to the new slot (the LDS load below reads
+      // the old one): an overflow in this class leaves it there for the
+      // next round
+      const GKRec* __restrict__ osrc = gk_table_ptr_cs(st, s, scls, sslot);
+      GKRec* __restrict__ odst = st.tab[lcls] + (int64_t)slot * st.cap[lcls];
+      const int oE = min(E, st.cap[scls]);
+      for (int j = lane; j < oE; j += 64) odst[j] = osrc[j];
+      if (lane == 0) {
+        st.cls[s] = lcls;
+        st.slot[s] = slot;
+        pool.list[lcls][atomicAdd(&pool.ctr[GK_CTR_LCNT + lcls], 1)] = (int32_t)s;
+      }
+      ucls = lcls;
+      uslot = slot;
+    } else if (scls != lcls) {
+      continue;  // in another class: handled by that class's launch
+    }
     // a promoted stream continues from value n - n0 of the call (the flushes
     // its smaller class made before overflowing are committed: k_ingest_small)
     const int64_t xo = xo0 + ((lcls > 0 && x) ? n - rfl64(st.n0[s]) : 0);
@@ -1787,7 +1824,8 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
     // force 2: unconditional merge_compress() (merge, gk:122, 126, 137)
     // a query launch (qs != NULL, force 1) answers every stream
     if (Lx <= 0 && !((force == 1 && p > 0) || (force == 2 && n > 0)) && !qs) continue;
-    GKRec* __restrict__ tab = gk_table_ptr_cs(st, s, scls, sslot);
+    GKRec* __restrict__ tab = gk_table_ptr_cs(st, s, ucls, uslot);
+    const GKRec* __restrict__ ltab = gk_table_ptr_cs(st, s, scls, sslot);  // (pre-call table: tab unless just promoted)
     double* __restrict__ pb = st.pbuf + s * (int64_t)st.pmax;
     int cur = 0;
     // table -> LDS: all of a lane's loads are issued before the first wait
@@ -1797,7 +1835,7 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
 #pragma unroll
       for (int r = 0; r < TL; ++r) {
         const int j = j0 + lane + 64 * r;
-        if (j < E) rc[r] = tab[j];
+        if (j < E) rc[r] = ltab[j];
       }
 #pragma unroll
       for (int r = 0; r < TL; ++r) {
@@ -1897,9 +1935,17 @@ __global__ __launch_bounds__(64) void k_ingest(GKState st, const double* __restr
     if (!ok) {
       // nothing was written back: the stream keeps its pre-call state and
       // is re-run by the host after promotion to the next capacity class
+      // (past the last class: counted fatal, as k_promote_dev would)
       if (lane == 0) {
-        const int k = atomicAdd(ovf_count, 1);
-        ovf_list[k] = (int32_t)s;
+        if (pmode & 2) {
+          atomicAdd(&pool.ctr[GK_CTR_FATAL], 1);
+          atomicMax(&pool.ctr[GK_CTR_FATAL + 1], (int)s);
+        } else if (pmode & 4) {
+          pool.defer[atomicAdd(&pool.ctr[GK_CTR_DEFER], 1)] = (int32_t)s;
+        } else {
+          const int k = atomicAdd(ovf_count, 1);
+          ovf_list[k] = (int32_t)s;
+        }
       }
       wsync<CAP == 0>();
       continue;
@@ -5253,7 +5299,8 @@ static hipError_t launch_ingest_t(const GKState& st, const double* x, const int6
                                   unsigned char* ws, size_t ws_bytes, int64_t ws_blocks,
                                   int32_t* ovf_count, int32_t* ovf_list, const GKQuery& q,
                                   unsigned long long* work, const int32_t* prio, const int32_t* prio_count,
-                                  const double* psort, const int64_t* prio_ws, const int32_t* prio_skip, hipStream_t stream) {
+                                  const double* psort, const int64_t* prio_ws, const int32_t* prio_skip, hipStream_t stream,
+                                  const GKPoolDev& pool, int pmode) {
   if (count <= 0 && !count_ptr) return hipSuccess;
   if (!work) return hipErrorInvalidValue;
   int64_t grid;
@@ -5274,7 +5321,7 @@ static hipError_t launch_ingest_t(const GKState& st, const double* x, const int6
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL((k_ingest<CAP, VPL>), dim3((unsigned)grid), dim3(64), 0, stream, st, x, offs, list,
                      count, count_ptr, lcls, force, cap, ws, ws_bytes, ovf_count, ovf_list, q.qs, q.nq, q.out,
-                     q.mode, work, prio, prio_count, psort, prio_ws, prio_skip);
+                     q.mode, work, prio, prio_count, psort, prio_ws, prio_skip, pool, pmode);
   return hipGetLastError();
 }
 
@@ -5285,9 +5332,10 @@ static hipError_t launch_ingest_vpl(int vpl, const GKState& st, const double* x,
                                     size_t ws_bytes, int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list,
                                     const GKQuery& q, unsigned long long* work, const int32_t* prio,
                                     const int32_t* prio_count, const double* psort, const int64_t* prio_ws, const int32_t* prio_skip,
-                                    hipStream_t stream) {
+                                    hipStream_t stream, const GKPoolDev& pool, int pmode) {
 #define GK_L(V) launch_ingest_t<CAP, V>(st, x, offs, list, count, count_ptr, lcls, force, cap, ws, ws_bytes, ws_blocks, \
-                                        ovf_count, ovf_list, q, work, prio, prio_count, psort, prio_ws, prio_skip, stream)
+                                        ovf_count, ovf_list, q, work, prio, prio_count, psort, prio_ws, prio_skip, stream, \
+                                        pool, pmode)
   switch (vpl) {
     case 1: return GK_L(1);
     case 2: return GK_L(2);
@@ -5362,10 +5410,14 @@ hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x
                             int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list, const GKQuery& q,
                             unsigned long long* work, const int32_t* prio, const int32_t* prio_count,
                             const double* psort, const int64_t* prio_ws, const int32_t* prio_skip, int fused_stats,
-                            hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop) {
+                            hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop, const GKPoolDev* pool,
+                            int pmode) {
+  const GKPoolDev nopool{};
+  const GKPoolDev& pl = pool ? *pool : nopool;
+  if (pmode && !pool) return hipErrorInvalidValue;
   switch (cap) {
     case SMALL_CAP:
-      if (list || count_ptr || lcls != 0) return hipErrorInvalidValue;  // class 0 over every stream only
+      if (list || count_ptr || lcls != 0 || pmode) return hipErrorInvalidValue;  // class 0 over every stream only
       if (vpl == 1)
         return launch_ingest_small<1>(st, x, offs, list, count, force, ovf_count, ovf_list, q, work, fused_stats, stream,
                                       ev_start, ev_stop);
@@ -5375,11 +5427,13 @@ hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x
       return hipErrorInvalidValue;
     case 2048:
       return launch_ingest_vpl<2048>(vpl, st, x, offs, list, count, count_ptr, lcls, force, cap, nullptr, 0, 0,
-                                     ovf_count, ovf_list, q, work, prio, prio_count, psort, prio_ws, prio_skip, stream);
+                                     ovf_count, ovf_list, q, work, prio, prio_count, psort, prio_ws, prio_skip, stream,
+                                     pl, pmode);
     default:
       if (!ws || ws_blocks <= 0) return hipErrorInvalidValue;
       return launch_ingest_vpl<0>(vpl, st, x, offs, list, count, count_ptr, lcls, force, cap, ws, ws_bytes,
-                                  ws_blocks, ovf_count, ovf_list, q, work, prio, prio_count, psort, prio_ws, prio_skip, stream);
+                                  ws_blocks, ovf_count, ovf_list, q, work, prio, prio_count, psort, prio_ws, prio_skip, stream,
+                                  pl, pmode);
   }
 }
 

@@ -57,10 +57,12 @@ hipError_t gk_launch_ingest(int cap, int vpl, const GKState& st, const double* x
                             int64_t ws_blocks, int32_t* ovf_count, int32_t* ovf_list, const GKQuery& q,
                             unsigned long long* work, const int32_t* prio, const int32_t* prio_count,
                             const double* psort, const int64_t* prio_ws, const int32_t* prio_skip, int fused_stats,
-                            hipStream_t stream, hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
+                            hipStream_t stream, hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr,
+                            const struct GKPoolDev* pool = nullptr, int pmode = 0);
 // (ev_start / ev_stop: the small-class launch records them as part of its
 // dispatch -- hipExtLaunchKernel, the kernel's own start and end -- instead of
-// two marker packets around it; other classes ignore them)
+// two marker packets around it; other classes ignore them.  pool / pmode:
+// the promotion rounds' fused steps, k_ingest's pmode)
 // The unbounded class (tables beyond 32768 entries; every class when P > 1024):
 // one wave per stream over ws (ws_bytes >= gk_big_ws_bytes(cap, P) per block,
 // ws_blocks blocks); list / count / count_ptr / lcls / force / q as above;
