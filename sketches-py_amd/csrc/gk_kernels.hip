@@ -3235,7 +3235,12 @@ __global__ __launch_bounds__(64) void k_ingest_big(GKState st, const double* __r
 // ((g, d) packed in 32 bits, T one flush ahead, selective
 // count zeroing, masked in-gap rank reads, every batch register-sorted).
 #ifndef GK_SMALL_WAVES
-#define GK_SMALL_WAVES 6  // min waves per SIMD asked of the register allocator
+// min waves per SIMD asked of the register allocator: 7 (72 VGPRs) since
+// round 6 -- the round-6 flush fits without a spill inside the flush loop
+// (the few left are per stream and per stats batch), and the seventh wave
+// hides latency: cfg3 launch 5.54 -> 5.35 ms (profiles/r06/r07a_*; round 2's
+// 7-wave build spilled in the flush and lost)
+#define GK_SMALL_WAVES 7
 #endif
 // largest gap handled by the in-gap rank loop; larger gaps rank by counting
 #ifndef GK_SMALL_RANK_MAX
@@ -5354,20 +5359,28 @@ static hipError_t launch_ingest_small(const GKState& st, const double* x, const 
                                       hipStream_t stream, hipEvent_t ev0, hipEvent_t ev1) {
   if (count <= 0) return hipSuccess;
   if (!work) return hipErrorInvalidValue;
-  static std::atomic<int> occ_cache[GK_MAX_DEV];  // (queried once per device)
+  // (queried once per device, for each of the two kernels: their register
+  // counts may differ)
+  static std::atomic<int> occ_cache[GK_MAX_DEV], occ_cache_fs[GK_MAX_DEV];
   const int occ = per_device(occ_cache, [](int) {
     int o = 0;
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_ingest_small<VPL, false>, 64, 0);
     return o;
   });
+  const int occ_fs = per_device(occ_cache_fs, [](int) {
+    int o = 0;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_ingest_small<VPL, true>, 64, 0);
+    return o;
+  });
+  const bool fs_launch = fused_stats > 0 && x && !list;
   // one resident wave per slot; streams are handed out through `work`
-  int64_t grid = (int64_t)num_cu() * occ;
+  int64_t grid = (int64_t)num_cu() * (fs_launch ? occ_fs : occ);
   if (grid > count) grid = count;
   if (grid < 1) grid = 1;
   // stats role: fused_stats/8 waves per CU start with the _sum/_avg chains
   // (only for the batch launch over every stream: x given, no list)
   int nstat = 0;
-  if (fused_stats > 0 && x && !list) {
+  if (fs_launch) {
     const int64_t want = std::max<int64_t>(1, (int64_t)num_cu() * fused_stats / 8);  // eighths of a wave per CU
     nstat = (int)(grid < want ? grid : want);
   }
