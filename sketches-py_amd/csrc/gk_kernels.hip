@@ -3340,8 +3340,12 @@ __device__ __forceinline__ void small_zero_counts(int2* gi, int lane) {
   gk_v4u z;
   __asm__ volatile("v_mov_b64 %0, 0" : "=v"(z.xy));
   __asm__ volatile("v_mov_b64 %0, 0" : "=v"(z.zw));
-  ((gk_v4u*)gi)[lane] = z;                                // records 0..127
-  ((uint2*)gi)[128 + (lane & 7)] = make_uint2(z.x, z.y);  // records 128..135
+  // (lane & 7 made opaque: hoisted out of the stream loop, its address was
+  // spilled at 8 waves per SIMD and reloaded from scratch every flush)
+  int l7 = lane & 7;
+  __asm__ volatile("" : "+v"(l7));
+  ((gk_v4u*)gi)[lane] = z;                          // records 0..127
+  ((uint2*)gi)[128 + l7] = make_uint2(z.x, z.y);  // records 128..135
 }
 
 __device__ __forceinline__ void small_pad(double* tv, int E, int lane) {
