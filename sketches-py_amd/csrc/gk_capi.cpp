@@ -130,6 +130,7 @@ struct gk_set {
   // this stream beside the ingest launches; ev_fork / ev_join order it
   hipStream_t aux = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_slgo = nullptr;  // aux has passed the fork: k_stats_long is next there
   // presorted flush batches of long streams (sets whose class 0 is the 2048
   // class): plan arrays, workspace, and the size the last call needed
   GKPresort ps;
@@ -335,7 +336,7 @@ void poll(gk_set* h, bool block) {
 
 int promote_rounds(gk_set* h, const double* x, const int64_t* offs, int force, const GKQuery& q, hipStream_t s,
                    bool fresh = false);
-int mark_done(gk_set* h, hipStream_t s);
+int mark_done(gk_set* h, hipStream_t s, bool ingest = false);
 
 // Start of a call's device work: ONE memset zeroes every per-call counter
 // (deferred / long-stream counts, re-run and overflow list lengths, the
@@ -481,8 +482,13 @@ int take_sticky(gk_set* h) {
 }
 
 // End of a call's device work on `s`: counters -> pinned host memory.
-int mark_done(gk_set* h, hipStream_t s) {
-  HIP_TRY(hipMemcpyAsync(h->h_ctr, h->d_ctr, GK_CTR_WORDS * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+// (ingest: the call listed the long streams -- word GK_CTR_LONG comes back
+// too; every other call leaves the host copy of the last ingest's count, which
+// stats_fork's fork decision reads)
+static_assert(GK_CTR_LONG == GK_CTR_WORDS - 1, "the long-stream count is the last word read back");
+int mark_done(gk_set* h, hipStream_t s, bool ingest) {
+  HIP_TRY(hipMemcpyAsync(h->h_ctr, h->d_ctr, (GK_CTR_WORDS - (ingest ? 0 : 1)) * sizeof(int32_t),
+                         hipMemcpyDeviceToHost, s));
   if (h->ps.wg_count && h->wg_trace)
     HIP_TRY(hipMemcpyAsync(h->h_ctr + GK_CTR_WORDS, h->ps.wg_count, sizeof(int32_t), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipEventRecord(h->ev_done, s));
@@ -821,8 +827,8 @@ int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s, i
   }
   const bool presort = h->ps.list_ws && h->ps.ws && h->ps.ws_cap > 0;
   // No fork when nothing but k_stats_long would go to the aux streams and the
-  // set's last completed call listed no long stream (its counter words come
-  // back with every call): k_stats_long then runs on `s` behind the ingest
+  // set's last ingest call listed no long stream (its count comes back with
+  // that call's counters): k_stats_long then runs on `s` behind the ingest
   // (stats_join).  Forked, its workgroups must reach the CUs before the
   // persistent ingest grid -- the fork's cross-queue wake-up (~13 us) is then
   // on the step's critical path, and a k_stats_long dispatched beside the
@@ -846,14 +852,23 @@ int stats_fork(gk_set* h, const double* x, const int64_t* offs, hipStream_t s, i
                                 ovf_list(h, 0), wwork_early, h->ps, h->aux2, nullptr));
     HIP_TRY(hipEventRecord(h->ev_wg, h->aux2));
   }
+  // Forked ahead of the small-class launch (nothing else between them on
+  // `s`): `s` waits until aux has passed the fork, so that k_stats_long's
+  // waves reach the CUs before the persistent ingest grid -- dispatched beside
+  // it they ran 2x longer and slowed the ingest (cfg4 x 8 shards 79 -> 84 ms
+  // per step, profiles/r06/r07i_*).  Costs one cross-queue wake-up (~13 us)
+  // on calls that fork (long streams: steps of tens of ms).
+  const bool sl_order = !h->sl_inline && stats_fused(h) && !presort && !h->aux2;
   if (!h->sl_inline) {
     HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_fork, 0));
     h->forked = true;
+    if (sl_order) HIP_TRY(hipEventRecord(h->ev_slgo, h->aux));
     HIP_TRY(gk_launch_stats_long(h->st, x, offs, h->d_long_list, prep ? h->d_long_n : nullptr, h->d_long_count,
                                  hc_on ? h->d_hc_count : nullptr, h->aux));
     h->hc_active = hc_on;  // (stats_join hands the picked chains to the worker)
     HIP_TRY(hipEventRecord(h->ev_join, h->aux));
   }
+  if (sl_order) HIP_TRY(hipStreamWaitEvent(s, h->ev_slgo, 0));
   if (presort) {
     // with k_ingest_wg beside it (ps.done): on its own stream, joined by
     // stats_join; else on aux2 ahead of k_ingest_wg
@@ -1264,6 +1279,7 @@ int gk_create(int64_t num_streams, double eps, int64_t cap_hint, int device, gk_
   if (h->P > 128 && !h->big[0]) okm &= hipStreamCreateWithFlags(&h->aux2, hipStreamNonBlocking) == hipSuccess;
   okm &= hipEventCreateWithFlags(&h->ev_presort, hipEventDisableTiming) == hipSuccess;
   okm &= hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) == hipSuccess;
+  okm &= hipEventCreateWithFlags(&h->ev_slgo, hipEventDisableTiming) == hipSuccess;
   okm &= hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) == hipSuccess;
   okm &= hipMalloc(&h->d_hc, GK_HC_MAX * sizeof(GKHostChainRec)) == hipSuccess;
   okm &= hipMalloc(&h->d_hc_count, sizeof(int32_t)) == hipSuccess;
@@ -1349,7 +1365,7 @@ int gk_destroy(gk_set* h) {
     if (h->d_ovfl[r]) (void)hipFree(h->d_ovfl[r]);
   for (auto* v : {&h->tev_flush, &h->tev_stats})
     for (hipEvent_t e : *v) (void)hipEventDestroy(e);
-  for (hipEvent_t e : {h->ev_fork, h->ev_join, h->ev_done, h->ev_qs, h->ev_hc})
+  for (hipEvent_t e : {h->ev_fork, h->ev_join, h->ev_slgo, h->ev_done, h->ev_qs, h->ev_hc})
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : h->hc_ev) (void)hipEventDestroy(e);
   if (h->hc_copy) (void)hipStreamDestroy(h->hc_copy);
@@ -1411,7 +1427,7 @@ int gk_ingest(gk_set* h, const double* values, const int64_t* offsets, void* str
   }
   rc = run_ingest(h, values, offsets, 0, s, GKQuery(), true);
   const int rj = stats_join(h, s, GKQuery());  // joined on every path
-  const int rd = mark_done(h, s);
+  const int rd = mark_done(h, s, true);
   return rc ? rc : (rj ? rj : rd);
 }
 
@@ -1531,7 +1547,7 @@ int gk_ingest_quantiles(gk_set* h, const double* values, const int64_t* offsets,
   // leftover pending values and answer from the LDS-resident table
   rc = run_ingest(h, values, offsets, 1, s, q, true);
   const int rj = stats_join(h, s, q);  // joined on every path
-  const int rd = mark_done(h, s);
+  const int rd = mark_done(h, s, true);
   return rc ? rc : (rj ? rj : rd);
 }
 

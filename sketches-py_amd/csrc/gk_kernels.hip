@@ -4410,8 +4410,8 @@ __device__ unsigned long long gk_tl_wave[5 * GK_TL_MAXW];
 __device__ unsigned long long gk_tl_sbeg[GK_TL_MAXS];
 __device__ unsigned long long gk_tl_send[GK_TL_MAXS];
 #endif
-template <int VPL, bool FS>
-__global__ __launch_bounds__(64, GK_SMALL_WAVES) void k_ingest_small(GKState st, const double* __restrict__ x,
+template <int VPL, bool FS, int W = GK_SMALL_WAVES>
+__global__ __launch_bounds__(64, W) void k_ingest_small(GKState st, const double* __restrict__ x,
                                                      const int64_t* __restrict__ offs, int64_t count, int force,
                                                      int32_t* __restrict__ ovf_count, int32_t* __restrict__ ovf_list,
                                                      const double* __restrict__ qs, int nq,
@@ -5363,24 +5363,40 @@ static hipError_t launch_ingest_small(const GKState& st, const double* x, const 
                                       hipStream_t stream, hipEvent_t ev0, hipEvent_t ev1) {
   if (count <= 0) return hipSuccess;
   if (!work) return hipErrorInvalidValue;
-  // (queried once per device, for each of the two kernels: their register
-  // counts may differ)
-  static std::atomic<int> occ_cache[GK_MAX_DEV], occ_cache_fs[GK_MAX_DEV];
-  const int occ = per_device(occ_cache, [](int) {
-    int o = 0;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_ingest_small<VPL, false>, 64, 0);
-    return o;
-  });
-  const int occ_fs = per_device(occ_cache_fs, [](int) {
-    int o = 0;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_ingest_small<VPL, true>, 64, 0);
-    return o;
-  });
   const bool fs_launch = fused_stats > 0 && x && !list;
+  // Two builds of each kernel: GK_SMALL_WAVES (7) waves per SIMD, and 6 for
+  // launches of few streams per wave (occupancy queried once per device and
+  // kernel: the register counts may differ).
+  static std::atomic<int> occ_cache[2][2][GK_MAX_DEV];
+  auto occ_of = [&](bool fs, bool w6) -> int {
+    return per_device(occ_cache[fs][w6], [fs, w6](int) {
+      int o = 0;
+      if (fs) {
+        if (w6) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_ingest_small<VPL, true, 6>, 64, 0);
+        else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_ingest_small<VPL, true>, 64, 0);
+      } else {
+        if (w6) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_ingest_small<VPL, false, 6>, 64, 0);
+        else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k_ingest_small<VPL, false>, 64, 0);
+      }
+      return o;
+    });
+  };
   // one resident wave per slot; streams are handed out through `work`
-  int64_t grid = (int64_t)num_cu() * (fs_launch ? occ_fs : occ);
-  if (grid > count) grid = count;
-  if (grid < 1) grid = 1;
+  auto full_grid = [&](bool w6) -> int64_t {
+    int64_t g = (int64_t)num_cu() * occ_of(fs_launch, w6);
+    return std::max<int64_t>(1, std::min<int64_t>(g, count));
+  };
+  // Few streams per wave (cfg4: 10^4 streams of 10^6 values, 1.4 per wave at
+  // 7 waves per SIMD): the launch lasts a wave's share of streams, and the
+  // 6-wave build runs each faster (cfg4 80.4 -> 71.2 ms per step); many
+  // (cfg3: 140 per wave) -- the 7-wave build's latency hiding wins
+  // (profiles/r06/r07_waves_per_simd_ab.txt).  GK_SMALL_W=6|7 forces one.
+  static const int w_env = getenv("GK_SMALL_W") ? atoi(getenv("GK_SMALL_W")) : 0;
+  static const int few_rounds = getenv("GK_FEW_ROUNDS") ? atoi(getenv("GK_FEW_ROUNDS")) : 4;
+  int64_t grid = full_grid(false);
+  const int64_t rounds7 = (count + grid - 1) / grid;
+  const bool w6 = w_env ? w_env == 6 : (GK_SMALL_WAVES != 6 && rounds7 <= few_rounds);
+  if (w6) grid = full_grid(true);
   // stats role: fused_stats/8 waves per CU start with the _sum/_avg chains
   // (only for the batch launch over every stream: x given, no list)
   int nstat = 0;
@@ -5394,12 +5410,17 @@ static hipError_t launch_ingest_small(const GKState& st, const double* x, const 
   if (list) return hipErrorInvalidValue;  // class 0 over every stream only
   // (ev0 / ev1: recorded by the dispatch itself -- the kernel's own start and
   // end -- when given)
-  if (nstat > 0)
-    hipExtLaunchKernelGGL((k_ingest_small<VPL, true>), dim3((unsigned)grid), dim3(64), 0, stream, ev0, ev1, 0, st, x,
-                          offs, count, force, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode, work, nstat, pace, lag);
-  else
-    hipExtLaunchKernelGGL((k_ingest_small<VPL, false>), dim3((unsigned)grid), dim3(64), 0, stream, ev0, ev1, 0, st, x,
-                          offs, count, force, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode, work, nstat, pace, lag);
+#define GK_SMALL_LAUNCH(FS_, W_)                                                                              \
+  hipExtLaunchKernelGGL((k_ingest_small<VPL, FS_, W_>), dim3((unsigned)grid), dim3(64), 0, stream, ev0, ev1, 0, st, x, \
+                        offs, count, force, ovf_count, ovf_list, q.qs, q.nq, q.out, q.mode, work, nstat, pace, lag)
+  if (nstat > 0) {
+    if (w6) GK_SMALL_LAUNCH(true, 6);
+    else GK_SMALL_LAUNCH(true, GK_SMALL_WAVES);
+  } else {
+    if (w6) GK_SMALL_LAUNCH(false, 6);
+    else GK_SMALL_LAUNCH(false, GK_SMALL_WAVES);
+  }
+#undef GK_SMALL_LAUNCH
   return hipGetLastError();
 }
 
