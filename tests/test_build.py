@@ -52,30 +52,33 @@ def small_isa(tmp_path_factory):
 
 def test_fast_class_has_no_scratch(resource_report, small_isa):
     """The small class runs nearly every stream: no scratch traffic in the
-    per-flush path.  The allocator folds a few loop-invariant per-lane LDS /
-    global addresses into scratch: stored once at kernel entry, reloaded once
-    per stream (end-of-stream pending copy, the empty-table first flush).
-    Keeping them in registers instead (e.g. re-reading the gap info at emit)
-    measured 1-2% slower (profiles/archive/r01t_ab_regpressure_REJECTED.txt), so the
-    bound is on the count: a spill inside the flush loops adds many more.
-    The stats role (fused_stats_role, run by a few waves before they join the
-    hand-out) adds one more folded value (48 bytes, 11 scratch instructions
-    at most); the ingest-only launch measured the same with and without it
-    (GK_FUSED_STATS=0 rows of profiles/archive/r01z_ab_fused_stats.txt).
-    The VPL=1 instance (P <= 64) carries more since the DPP lane exchanges
-    (profiles/r02k_dpp_exchanges_sq.txt: one 4-byte reload per flush) and the
-    paced stats role (per-batch reloads of its part bounds,
-    profiles/r02y_stats_pacing_ab.txt).
-    Since v18 the stats role is a template flag (4 instances: VPL 1/2, with
-    and without the role); the bench's instance (VPL=2 with the role, 5.90 ms
-    per cfg3 launch at 23 scratch instructions) sets the bounds."""
+    per-flush path.  The allocator folds a few loop-invariant per-lane
+    addresses into scratch, stored at kernel entry and reloaded per stream or
+    per stats batch (loop depth <= 1 in the ISA's loop annotations); a spill
+    inside the flush loop (depth >= 2) costs a memory round trip per flush
+    and fails this test.  Since round 6 every (VPL, stats role) instance is
+    built twice, for 7 waves per SIMD (72 VGPRs, the product) and for 6 (80
+    VGPRs: launches of few streams per wave), 8 instances; the 7-wave
+    stats-role instances carry the most (<= 40 scratch instructions, all per
+    stream / per batch: profiles/r06/r07_waves_per_simd_ab.txt)."""
     fast = {k: v for k, v in resource_report.items() if k.startswith("_Z14k_ingest_small")}
-    assert len(fast) == 4
+    assert len(fast) == 8
     for k, v in fast.items():
-        assert v.get("ScratchSize [bytes/lane]", 0) <= 64, (k, v)
+        assert v.get("ScratchSize [bytes/lane]", 0) <= 96, (k, v)
     for name, body in small_isa.items():
-        ops = re.findall(r"^\s*(scratch_\w+)", body, re.M)
-        assert len(ops) <= 24, (name, ops)
+        depth = 0
+        inner = []
+        total = 0
+        for line in body.splitlines():
+            if line.startswith(".LBB") or line.startswith("; %bb"):
+                m = re.search(r"Loop: Header=\S+ Depth=(\d+)", line)
+                depth = int(m.group(1)) if m else 0
+            if re.match(r"^\s*scratch_\w+", line):
+                total += 1
+                if depth >= 2:
+                    inner.append(line.strip())
+        assert not inner, (name, inner)
+        assert total <= 40, (name, total)
 
 
 def test_no_inline_asm_memory_ops():
@@ -88,6 +91,11 @@ def test_no_inline_asm_memory_ops():
 
 
 def test_fast_class_occupancy(resource_report):
-    k = [v for n, v in resource_report.items() if n.startswith("_Z14k_ingest_smallILi2E")][0]
-    assert k["Occupancy [waves/SIMD]"] >= 4
-    assert k["LDS Size [bytes/block]"] <= 9 * 1024
+    """The 7-wave build reaches 7 waves per SIMD (the persistent grid assumes
+    it), the 6-wave build 6; LDS stays small enough for 7 x 4 waves per CU."""
+    ks = {n: v for n, v in resource_report.items() if n.startswith("_Z14k_ingest_smallILi2E")}
+    assert ks
+    for n, k in ks.items():
+        want = 7 if "Li7E" in n else 6
+        assert k["Occupancy [waves/SIMD]"] >= want, (n, k)
+        assert k["LDS Size [bytes/block]"] * 28 <= 160 * 1024, (n, k)
