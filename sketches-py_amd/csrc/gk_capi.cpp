@@ -972,7 +972,7 @@ int promote_rounds(gk_set* h, const double* x, const int64_t* offs, int force, c
     // k_promote_dev launch and no re-run list.  GK_PROMOTE_FUSE=0: always the
     // separate promotion.
     const int c_end = fresh ? std::min(r + 1, R) : R;
-    static const bool fuse_env = !getenv("GK_PROMOTE_FUSE") || atoi(getenv("GK_PROMOTE_FUSE")) != 0;
+    const bool fuse_env = !getenv("GK_PROMOTE_FUSE") || atoi(getenv("GK_PROMOTE_FUSE")) != 0;  // (per call: A/B, tests)
     bool fuse = fuse_env && r < R;
     for (int c = r; c < c_end; ++c) fuse = fuse && h->st.alloc[c] > 0 && !h->big[c];
     if (fuse) {

@@ -160,6 +160,54 @@ def test_small_class_partial_commit_then_promotion(gpu_device, monkeypatch, caps
     check_q(ss, o, eps, "partial commit " + caps)
 
 
+@pytest.mark.parametrize("fuse,fork", [("1", False), ("0", False), ("1", True)])
+def test_round6_call_paths_vs_oracle(gpu_device, monkeypatch, fuse, fork):
+    """Round-6 call paths, bit-exact against the oracle after every call:
+    promotion rounds fused into the class re-run launches (GK_PROMOTE_FUSE=1,
+    the default) or as separate k_promote_dev launches (0), over a ladder
+    of four classes (128 -> 256 -> 512 -> 4096: several rounds per call) and across calls
+    (member-list launches, non-fresh rounds); streams longer than 16 384
+    values in the small class (k_stats_long) with the fork decided by the
+    last ingest's count (first call: behind the ingest on the call's stream)
+    or always forked (GK_SL_FORK=1); a reset between calls (k_reset zeroes
+    the per-call counters, the next call skips its memset)."""
+    monkeypatch.setenv("GK_CAPS", "128,256,512,4096")
+    monkeypatch.setenv("GK_PROMOTE_FUSE", fuse)
+    if fork:
+        monkeypatch.setenv("GK_SL_FORK", "1")
+    else:
+        monkeypatch.delenv("GK_SL_FORK", raising=False)
+    eps = 0.01
+    rng = np.random.default_rng(29)
+    S = 40
+
+    def batch(k):
+        seqs = []
+        for i in range(S):
+            kind = (i + k) % 5
+            if kind == 0:
+                seqs.append(desc(int(rng.integers(20000, 60000))) - 1e6 * k)  # promoted, long
+            elif kind == 1:
+                seqs.append(rng.pareto(1.5, int(rng.integers(17000, 40000))) + 1)  # long stats chain
+            elif kind == 2:
+                seqs.append(rng.random(int(rng.integers(0, 3000))))
+            elif kind == 3:
+                seqs.append(np.zeros(int(rng.integers(0, 300))))
+            else:
+                seqs.append(rng.lognormal(0, 2, int(rng.integers(100, 9000))))
+        return seqs
+
+    ss = _ss(S, eps, gpu_device)
+    o = OracleSet(S, eps)
+    run_batches(ss, o, [batch(0), batch(1)], "round-6 paths fuse=%s fork=%s" % (fuse, fork))
+    assert ss.num_promoted >= 8
+    check_q(ss, o, eps, "round-6 paths")
+    ss.reset()
+    o = OracleSet(S, eps)
+    run_batches(ss, o, [batch(2), batch(3)], "round-6 paths after reset")
+    check_q(ss, o, eps, "round-6 paths after reset")
+
+
 def test_small_class_fatal_stream_keeps_committed_prefix(gpu_device, monkeypatch):
     """A stream that outgrows every class (GK_CAPS=128,256: no unbounded
     class) is reported (sticky GK_E_OVERFLOW); what it keeps is the state
