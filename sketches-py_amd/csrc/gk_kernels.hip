@@ -2140,7 +2140,9 @@ __device__ __forceinline__ void wg_sort(WgLDS& L, double (&xv)[GK_WG_VPT], int c
 #ifndef GK_WG_EMIT_MAX
 #define GK_WG_EMIT_MAX 16
 #endif
+#ifndef GK_WG_EMIT_U
 #define GK_WG_EMIT_U 4
+#endif
 // KM: table entries per thread, >= ceil(E / GK_WG_T) (2 up to 1024 entries)
 template <int KM>
 __device__ int flush_wg(WgLDS& L, const int cur, const int E, double (&xv)[GK_WG_VPT], const int cnt,
