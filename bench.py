@@ -573,6 +573,10 @@ def main():
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
                      "traffic_ratio": ratio, "traffic_source": traffic_src,
                      "bytes_per_launch": bytes_per_launch, "launch_ms": k_ms,
+                     "launch_ms_source": ("HIP events recorded by the small-class launch itself (hipExtLaunchKernel "
+                                          "start/stop), mean over the timed steps" if a.workload != "cfg5" else
+                                          "HIP event markers around the class-0 launch and k_ingest_wg beside it, "
+                                          "mean over the timed steps"),
                      "stats_kernel_ms": (stats_ms / max(launches, 1)
                                          if os.environ.get("GK_BENCH_STATS_TIMING") == "1" else None)},
         "library": _library_identity(),
